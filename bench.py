@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py — patched-forward prompts/sec on the Pythia-2.8B layer x head
+causal-indirect-effect sweep (BASELINE.json metric).
+
+One step = one full CIE sweep of ``--prompts`` label-shuffled 4-shot prompts
+(T = 15 tokens) over all 32 x 32 (layer, head) sites: the clean forward of the
+prompts plus 12 x 1024 patched forwards, each evaluated to the probability of
+the prompt's first answer token (scratch2.py:171-197), i.e. 12,288 units per
+GPU per step.  Weights are seeded synthetic Pythia-2.8B (no checkpoints
+offline), fp32 like the reference (TransformerLens default dtype).
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling — every rank
+sweeps its own prompts; the [L, H] CIE partial sums are all-reduced once per
+step (the mean over all prompts).  value = units of all ranks / max-rank time.
+
+Extra JSON objects: ``roofline`` (dominant kernel = fp32 MFMA GEMM, achieved
+from HIP events on the engine's launch stream), ``cpu_baseline`` (the CPU
+oracle running the reference's loop structure on a bounded sample, rank 0 at
+N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "patched-forward prompts/sec, Pythia-2.8B layer×head CIE sweep, 1–8 GPUs"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec (155 measured)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="pythia-2.8b")
+    ap.add_argument("--prompts", type=int, default=12, help="CIE prompts per GPU per step")
+    ap.add_argument("--kshot", type=int, default=4)
+    ap.add_argument("--extract", type=int, default=256, help="prompts for the (untimed) mean extraction")
+    ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
+    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, cfg, prompts, answers, mean):
+    """The oracle (fp32 CPU, TransformerLens semantics, one batch-1 hooked
+    forward per site — scratch2.py:181-194) on prompt 0 at layers {0, L/2,
+    L-1} x ``--cpu-sites`` heads; rate = sites / wall time."""
+    import tvr_amd
+    from oracle.hooked_pythia import HookedPythiaOracle, OracleConfig
+    from oracle import reference_experiments as R
+
+    t0 = time.time()
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
+    oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
+                                             cfg.rotary_dim, cfg.n_ctx), sd, tokenizer=None)
+    del sd
+    log(f"cpu baseline: oracle weights ready in {time.time() - t0:.1f}s")
+    layers = sorted({0, cfg.n_layers // 2, cfg.n_layers - 1})
+    heads = list(range(min(args.cpu_sites, cfg.n_heads)))
+    mean_cpu = mean.detach().cpu()
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    R.calculate_average_causal_indirect_effect(mean_cpu, [prompts[0]], [[answers[0]]], oracle,
+                                               layers=layers, heads=heads)
+    dt = time.perf_counter() - t0
+    n_sites = len(layers) * len(heads)
+    return {"value": n_sites / dt, "unit": "patched prompts/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle fp32 CPU (TransformerLens semantics, batch-1 hooked forward per site, "
+                       f"reference loop scratch2.py:181-194): prompt 0 (T={len(prompts[0])}), layers {layers} x "
+                       f"heads {heads} = {n_sites} sites + 1 clean forward in {dt:.1f}s on {threads} threads")}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import tvr_amd
+    from tvr_amd.experiments import causal_indirect_effect_sums, sum_last_z
+
+    cfg = tvr_amd.get_config(args.model)
+    t0 = time.time()
+    model = tvr_amd.Model.from_pretrained(args.model, device=dev, seed=0)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] {args.model} synthetic weights on {dev} in {time.time() - t0:.1f}s")
+
+    # --- mean head activations (a1), untimed: synthetic 6-shot prompts (T=28)
+    import random
+    random.seed(4321)
+    pairs = tvr_amd.tasks.synthetic_task(52, cfg.d_vocab, seed=7)
+    ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, pairs, "→", ",", args.extract, 6)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    zsum = sum_last_z(model, ex_prompts)
+    torch.cuda.synchronize()
+    te = time.perf_counter() - te
+    mean = model.project_heads(zsum) / len(ex_prompts)
+
+    prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
+    units_per_step = len(prompts) * cfg.n_layers * cfg.n_heads
+
+    def step():
+        cie = causal_indirect_effect_sums(mean, prompts, answers, model)
+        if world > 1:
+            dist.all_reduce(cie)
+        return cie
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cie = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    total_units = units_per_step * args.steps * world
+    value = total_units / elapsed
+
+    # --- roofline: one more (untimed) step with HIP events around every GEMM
+    model.profile(True)
+    step()
+    torch.cuda.synchronize()
+    st = model.profile_stats()
+    model.profile(False)
+    achieved = st["gemm_flops"] / (st["gemm_ms"] * 1e-3) / 1e12
+    T = len(prompts[0])
+    L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
+    P_l = 4 * d * d + 2 * d * cfg.d_mlp
+    # F_alg(site at layer l) = (L-1-l)(2 P_l T + 2 T(T+1) d) + 2 d V
+    f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "patched prompts/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded Pythia-2.8B-shaped weights, seeded single-token shuffled-label prompts)",
+        "config": {
+            "workload": f"{args.model} CIE sweep {L}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
+                        f"{args.kshot}-shot, T={T}",
+            "sites_per_step_per_gpu": units_per_step,
+            "parallelism": f"prompt-sharded x{world}, weights replicated, 1 all-reduce of [L,H] per step",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32)",
+            "achieved": round(achieved, 2),
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None,
+            "launches_per_step": st["gemm_launches"],
+            "avg_launch_gflop": round(st["gemm_flops"] / max(st["gemm_launches"], 1) / 1e9, 3),
+            "avg_launch_ms": round(st["gemm_ms"] / max(st["gemm_launches"], 1), 4),
+            "gemm_share_of_step": round(st["gemm_ms"] / (elapsed / args.steps * 1e3), 4),
+        },
+        "algorithmic": {
+            "gflop_per_site": round(f_alg / 1e9, 2),
+            "site_tflops": round(value / world * f_alg / 1e12, 2),
+            "extraction_prompts_per_s": round(len(ex_prompts) / te, 1),
+        },
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, cfg, prompts, answers, mean)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

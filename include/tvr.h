@@ -1,0 +1,195 @@
+/*
+ * tvr.h — C ABI of the MI355X-native task-vector / function-vector engine.
+ *
+ * The reference (IMMachinations/Task-Vector-Replication) drives every patched
+ * forward through TransformerLens from Python loops:
+ *   - extraction   scratch2.py:81-100   (run_with_cache + hook_result[0,-1])
+ *   - layer sweeps scratch2.py:107-150  (run_with_hooks, hook_attn_out[0,-1] += v)
+ *   - CIE sweep    scratch2.py:171-197  (run_with_hooks, hook_result[0,:,h] = mean)
+ *   - FV eval      scratch2.py:292-314  (run_with_hooks + top-k)
+ *   - resid patch  scratch.py:106-147   (cache surgery + forward(start_at_layer=L))
+ * There is no native FFI in the reference: its Python façade binds these
+ * entry points through ctypes.  Every entry point below
+ * replaces one of those loops with ONE batched launch sequence whose batch
+ * dimension enumerates patch sites.
+ *
+ * Conventions
+ *   - Host arrays: token ids, sequence lengths, targets and site records.
+ *   - Device arrays: weights, vectors and all outputs; owned by the caller
+ *     (PyTorch) and preallocated.  Traces and the activation workspace are
+ *     owned by the engine (allocated outside timed regions, reused).
+ *   - `stream` is a hipStream_t passed as void*; everything is enqueued on it
+ *     and nothing synchronises the host except tvr_*_create / destroy.
+ *   - Every function returns TVR_OK (0) or a negative error code; no C++
+ *     exception crosses the ABI.  tvr_last_error() explains the last failure
+ *     on the calling thread.
+ *   - All arithmetic is fp32 (the reference's TransformerLens default dtype).
+ */
+#ifndef TVR_H_
+#define TVR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TVR_ABI_VERSION 1
+
+enum tvr_status {
+  TVR_OK = 0,
+  TVR_ERR_INVALID = -1,     /* bad argument / shape (reference: ValueError) */
+  TVR_ERR_HIP = -2,         /* HIP runtime failure */
+  TVR_ERR_NOMEM = -3,       /* device allocation failed */
+  TVR_ERR_UNSUPPORTED = -4  /* shape outside what the kernels handle */
+};
+
+/* Patch-site kinds: the declarative replacement for TransformerLens hooks. */
+enum tvr_site_kind {
+  /* No patch: re-evaluate the clean last-position distribution. */
+  TVR_SITE_NONE = 0,
+  /* blocks.{layer}.attn.hook_result[0,:,head,:] = vectors[vec] at every
+   * position (scratch2.py:167-169, 187-189). */
+  TVR_SITE_REPLACE_HEAD_ALLPOS = 1,
+  /* blocks.{layer}.hook_attn_out[0,-1,:] += vectors[vec]
+   * (scratch2.py:107-109). */
+  TVR_SITE_ADD_ATTN_OUT_LASTPOS = 2,
+  /* blocks.{layer}.hook_resid_pre of sequence `seq` with row `pos` replaced by
+   * the same hook's row `src_pos` of sequence `src_seq`, then
+   * forward(start_at_layer=layer) (scratch.py:140-143, 201-209). */
+  TVR_SITE_SET_RESID_PRE_POS = 3
+};
+
+typedef struct tvr_config {
+  int32_t n_layers;
+  int32_t d_model;
+  int32_t n_heads;
+  int32_t d_head;
+  int32_t d_mlp;
+  int32_t d_vocab;
+  int32_t rotary_dim;
+  int32_t n_ctx;       /* rotary table length */
+  float ln_eps;
+  float rotary_base;
+} tvr_config;
+
+/* Per-layer weights after TransformerLens processing (fold_ln,
+ * center_writing_weights, fold_value_biases), in the engine's fused layout.
+ *   w1 [3*d_model + d_mlp][d_model]  rows: Q(head,d_head) | K | V | MLP-in
+ *   b1 [3*d_model + d_mlp]           (V part is zero after fold_value_biases)
+ *   w2 [d_model][d_model + d_mlp]    cols: O(head,d_head) | MLP-out
+ *   b2 [d_model]                     b_O (with folded value bias) + b_out   */
+typedef struct tvr_layer_weights {
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* b2;
+} tvr_layer_weights;
+
+/* One patched forward = one (prompt, patch site) pair = one unit of the
+ * metric "patched-forward prompts/sec". */
+typedef struct tvr_site {
+  int32_t seq;      /* clean sequence (prompt) index in the trace */
+  int32_t kind;     /* enum tvr_site_kind */
+  int32_t layer;    /* hook layer */
+  int32_t head;     /* REPLACE_HEAD_ALLPOS */
+  int32_t pos;      /* SET_RESID_PRE_POS: patched position in `seq` (>= 0) */
+  int32_t src_seq;  /* SET_RESID_PRE_POS: sequence supplying the row */
+  int32_t src_pos;  /* SET_RESID_PRE_POS: position supplying the row */
+  int32_t vec;      /* row of `vectors` (REPLACE / ADD) */
+  int32_t target;   /* token whose probability is reported, -1: none */
+} tvr_site;
+
+typedef struct tvr_model tvr_model;
+typedef struct tvr_trace tvr_trace;
+
+const char* tvr_version(void);
+int32_t tvr_abi_version(void);
+const char* tvr_last_error(void);
+
+/* Replaces HookedTransformer.from_pretrained(...) (scratch.py:26,
+ * scratch2.py:26): binds processed device weights (caller keeps them alive). */
+int tvr_model_create(const tvr_config* cfg, const float* w_embed /*[V][d]*/,
+                     const tvr_layer_weights* layers /*[n_layers] host*/,
+                     const float* w_unembed_t /*[V][d]*/,
+                     const float* b_unembed /*[V]*/, tvr_model** out);
+int tvr_model_destroy(tvr_model* model);
+
+/* Clean-run trace: every layer's hook_resid_pre, attn.hook_z and the K/V
+ * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */
+int tvr_trace_create(tvr_model* model, int32_t max_seqs, int32_t max_tokens,
+                     tvr_trace** out);
+int tvr_trace_destroy(tvr_trace* trace);
+/* Copy a traced hook into a caller device buffer [n_tokens][d] (async on
+ * `stream`): what = TVR_TRACE_RESID_PRE gives blocks.{layer}.hook_resid_pre
+ * (layer == n_layers: the final residual), TVR_TRACE_Z blocks.{layer}.attn.hook_z. */
+enum tvr_trace_hook { TVR_TRACE_RESID_PRE = 0, TVR_TRACE_Z = 1 };
+int tvr_trace_read(const tvr_trace* trace, int32_t what, int32_t layer, float* dst,
+                   void* stream);
+int32_t tvr_trace_num_tokens(const tvr_trace* trace);
+
+/* Batched clean forward of n_seq prompts (ragged lengths, packed tokens).
+ * Replaces the per-prompt model.forward / run_with_cache calls
+ * (scratch2.py:96,143,183,297; scratch.py:127,132,137).
+ *   trace        may be NULL (no snapshots kept)
+ *   targets      host [n_seq] token ids or NULL; out_prob [n_seq] gets
+ *                softmax(logits[-1])[target]
+ *   out_topk     device [n_seq][topk] int32 (descending, lowest id on ties)
+ *   out_logits   device [n_seq][V] last-position logits, or NULL
+ *   capture_zsum device [n_layers][d] fp32: += hook_z at each prompt's last
+ *                position (the reduction of scratch2.py:97-98), or NULL   */
+int tvr_forward_clean(tvr_model* model, tvr_trace* trace, const int32_t* tokens,
+                      const int32_t* seq_lens, int32_t n_seq,
+                      const int32_t* targets, float* out_prob,
+                      int32_t* out_topk, int32_t topk, float* out_logits,
+                      float* capture_zsum, void* stream);
+
+/* Batched patch sweep over sites against a clean trace (the staircase: a site
+ * at layer l reuses the clean run's layers <= l and K/V prefix).  Replaces the
+ * per-site run_with_hooks loops (scratch2.py:122-125,145-148,185-194,301,311;
+ * scratch.py:140-145).
+ *   vectors  device [n_vectors][d]
+ *   out_prob device [n_sites], out_topk device [n_sites][topk],
+ *   out_logits device [n_sites][V] or NULL                                  */
+int tvr_patch_sweep(tvr_model* model, const tvr_trace* trace,
+                    const tvr_site* sites, int32_t n_sites,
+                    const float* vectors, int32_t n_vectors, float* out_prob,
+                    int32_t* out_topk, int32_t topk, float* out_logits,
+                    void* stream);
+
+/* out[l][h][:] = zsum[l][h*d_head:(h+1)*d_head] @ W_O[l,h]: turns the z-form
+ * capture into the hook_result form of scratch2.py:98 (sum over prompts). */
+int tvr_project_heads(tvr_model* model, const float* zsum /*[L][d]*/,
+                      float* out /*[L][H][d]*/, void* stream);
+
+/* Primitive kernels, exported for unit tests and tools. */
+/* C[M][N] = A[M][K] (row stride lda) @ W[N][K]^T (row stride ldw) + bias */
+int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw,
+                 const float* bias, float* C, int32_t ldc, int32_t M,
+                 int32_t N, int32_t K, void* stream);
+/* TransformerLens LayerNormPre over rows: (x - mean) / sqrt(var + eps) */
+int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
+                  int32_t rows, int32_t d, float eps, void* stream);
+
+/* Kernel timing (HIP events recorded on the launch stream around every GEMM
+ * launch while enabled).  tvr_profile_read synchronises the recorded events
+ * and returns totals since the last enable; used by bench.py for the
+ * roofline's achieved TFLOP/s of the dominant kernel. */
+typedef struct tvr_kernel_stats {
+  int64_t gemm_launches;
+  double gemm_flops;   /* algorithmic 2*M*N*K summed over launches */
+  double gemm_ms;      /* summed launch durations */
+  double gemm_bytes;   /* minimal operand bytes (A + W + C) summed */
+} tvr_kernel_stats;
+int tvr_profile_enable(tvr_model* model, int32_t on);
+int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);
+
+/* Bytes of engine workspace currently held by the model (diagnostics). */
+size_t tvr_workspace_bytes(const tvr_model* model);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TVR_H_ */

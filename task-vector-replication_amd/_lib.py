@@ -1,0 +1,128 @@
+"""ctypes binding of ``libtvr.so`` (the C ABI declared in include/tvr.h).
+
+The reference is Python, so its binding to a native engine is a ctypes stub
+(INTEGRATION.md).  Loading fails loudly: there is no CPU fallback anywhere in
+the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_NAME = "libtvr.so"
+LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+
+# enum tvr_status
+TVR_OK = 0
+TVR_ERR_INVALID = -1
+TVR_ERR_HIP = -2
+TVR_ERR_NOMEM = -3
+TVR_ERR_UNSUPPORTED = -4
+
+# enum tvr_trace_hook
+TRACE_RESID_PRE = 0
+TRACE_Z = 1
+
+# enum tvr_site_kind
+SITE_NONE = 0
+SITE_REPLACE_HEAD_ALLPOS = 1
+SITE_ADD_ATTN_OUT_LASTPOS = 2
+SITE_SET_RESID_PRE_POS = 3
+
+c_f32p = ctypes.c_void_p
+c_i32p = ctypes.c_void_p
+
+
+class CLayerWeights(ctypes.Structure):
+    _fields_ = [("w1", ctypes.c_void_p), ("b1", ctypes.c_void_p),
+                ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p)]
+
+
+class CSite(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_int32), ("kind", ctypes.c_int32), ("layer", ctypes.c_int32),
+                ("head", ctypes.c_int32), ("pos", ctypes.c_int32), ("src_seq", ctypes.c_int32),
+                ("src_pos", ctypes.c_int32), ("vec", ctypes.c_int32), ("target", ctypes.c_int32)]
+
+
+SITE_FIELDS = [f for f, _ in CSite._fields_]
+
+
+class CKernelStats(ctypes.Structure):
+    _fields_ = [("gemm_launches", ctypes.c_int64), ("gemm_flops", ctypes.c_double),
+                ("gemm_ms", ctypes.c_double), ("gemm_bytes", ctypes.c_double)]
+
+# name -> (restype, argtypes); every symbol include/tvr.h declares.
+SIGNATURES = {
+    "tvr_version": (ctypes.c_char_p, []),
+    "tvr_abi_version": (ctypes.c_int32, []),
+    "tvr_last_error": (ctypes.c_char_p, []),
+    "tvr_model_create": (ctypes.c_int, [ctypes.c_void_p, c_f32p, ctypes.POINTER(CLayerWeights),
+                                        c_f32p, c_f32p, ctypes.POINTER(ctypes.c_void_p)]),
+    "tvr_model_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tvr_trace_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "tvr_trace_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tvr_trace_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, c_f32p,
+                                      ctypes.c_void_p]),
+    "tvr_trace_num_tokens": (ctypes.c_int32, [ctypes.c_void_p]),
+    "tvr_forward_clean": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_i32p, c_i32p, ctypes.c_int32,
+                                         c_i32p, c_f32p, c_i32p, ctypes.c_int32, c_f32p, c_f32p,
+                                         ctypes.c_void_p]),
+    "tvr_patch_sweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                       c_f32p, ctypes.c_int32, c_f32p, c_i32p, ctypes.c_int32, c_f32p,
+                                       ctypes.c_void_p]),
+    "tvr_project_heads": (ctypes.c_int, [ctypes.c_void_p, c_f32p, c_f32p, ctypes.c_void_p]),
+    "tvr_gemm_f32": (ctypes.c_int, [c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, c_f32p, c_f32p,
+                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_void_p]),
+    "tvr_lnpre_f32": (ctypes.c_int, [c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]),
+    "tvr_workspace_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
+}
+
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load libtvr.so (cached).  Raises if it is missing: build it with
+    ``python __graft_entry__.py`` or ``make -C task-vector-replication_amd/csrc``."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise EngineError(f"{p} not found: the HIP engine is not built (no CPU fallback exists); "
+                          "run `make -C task-vector-replication_amd/csrc`")
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.tvr_abi_version() != 1:
+        raise EngineError("libtvr ABI mismatch")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    """Status code → exception, with the reference's error types: invalid
+    shapes raise ValueError (scratch2.py:172-175), the rest RuntimeError."""
+    if rc == TVR_OK:
+        return
+    msg = (load().tvr_last_error() or b"").decode(errors="replace")
+    if rc == TVR_ERR_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise EngineError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (None → NULL)."""
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,752 @@
+// engine.hip — runtime behind include/tvr.h.
+//
+// Owns the per-model rotary tables and activation workspace, plans batched
+// sweeps (the "staircase": sites sorted by entry layer so the active rows of
+// layer l are always a prefix of the activation buffer) and enqueues the
+// kernels of kernels.hpp / gemm_f32.hpp on the caller's stream.
+//
+// Reference loops replaced (see include/tvr.h for the per-entry-point map):
+// scratch2.py:81-100 (extraction), :114-150 (layer sweeps), :171-197 (CIE),
+// :292-314 (FV eval) and scratch.py:106-147 (residual patch sweep).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tvr.h"
+#include "gemm_f32.hpp"
+#include "kernels.hpp"
+
+using namespace tvr;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define TVR_HIP(expr)                                                           \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess)                                                       \
+      return fail(TVR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define TVR_TRY(expr)        \
+  do {                       \
+    int _rc = (expr);        \
+    if (_rc != TVR_OK) return _rc; \
+  } while (0)
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// Bump allocator over one device allocation.
+struct Carve {
+  size_t off = 0;
+  template <class T>
+  size_t take(size_t count) {
+    const size_t at = off;
+    off = align_up(off + count * sizeof(T));
+    return at;
+  }
+};
+
+// Pinned host staging for per-call metadata (descriptors, tokens).  Two
+// buffers used alternately; an event guards reuse.
+struct Staging {
+  void* buf[2] = {nullptr, nullptr};
+  size_t cap[2] = {0, 0};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};
+  int next = 0;
+};
+
+}  // namespace
+
+struct tvr_model {
+  tvr_config cfg{};
+  int D1 = 0;  // 3d + d_mlp
+  int K2 = 0;  // d + d_mlp
+  const float* w_embed = nullptr;
+  std::vector<tvr_layer_weights> layers;
+  const float* w_unembed_t = nullptr;
+  const float* b_unembed = nullptr;
+  float* rot_cos = nullptr;
+  float* rot_sin = nullptr;
+  const float** d_w2s = nullptr;
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  Staging staging;
+  // profiling (tvr_profile_enable): event pairs around GEMM launches
+  bool prof = false;
+  struct ProfRec { hipEvent_t a, b; double flops, bytes; };
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> prof_pool;
+};
+
+struct tvr_trace {
+  tvr_model* model = nullptr;
+  int max_seqs = 0, max_tokens = 0;
+  float* resid = nullptr;  // [L+1][max_tokens][d]
+  float* z = nullptr;      // [L][max_tokens][d]
+  float* qkv = nullptr;    // [L][max_tokens][3d]
+  std::vector<int> seq_off, seq_len;
+  int n_seq = 0, n_tokens = 0;
+};
+
+namespace {
+
+constexpr int kFinalChunk = 1024;
+
+int ensure_workspace(tvr_model* m, size_t bytes, hipStream_t st) {
+  if (bytes <= m->ws_bytes) return TVR_OK;
+  TVR_HIP(hipStreamSynchronize(st));
+  if (m->ws) TVR_HIP(hipFree(m->ws));
+  m->ws = nullptr;
+  m->ws_bytes = 0;
+  const size_t want = align_up(bytes + bytes / 8);
+  if (hipMalloc(&m->ws, want) != hipSuccess) {
+    m->ws = nullptr;
+    (void)hipGetLastError();
+    return fail(TVR_ERR_NOMEM, "workspace allocation of " + std::to_string(want) + " bytes failed");
+  }
+  m->ws_bytes = want;
+  return TVR_OK;
+}
+
+// Copy host bytes to device through pinned staging (async on `st`).
+int upload(tvr_model* m, hipStream_t st, void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return TVR_OK;
+  Staging& s = m->staging;
+  const int i = s.next;
+  s.next ^= 1;
+  if (s.pending[i]) {
+    TVR_HIP(hipEventSynchronize(s.done[i]));
+    s.pending[i] = false;
+  }
+  if (s.cap[i] < bytes) {
+    if (s.buf[i]) TVR_HIP(hipHostFree(s.buf[i]));
+    s.buf[i] = nullptr;
+    const size_t want = align_up(std::max(bytes, (size_t)1 << 20));
+    TVR_HIP(hipHostMalloc(&s.buf[i], want, hipHostMallocDefault));
+    s.cap[i] = want;
+  }
+  if (!s.done[i]) TVR_HIP(hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming));
+  std::memcpy(s.buf[i], src, bytes);
+  TVR_HIP(hipMemcpyAsync(dst, s.buf[i], bytes, hipMemcpyHostToDevice, st));
+  TVR_HIP(hipEventRecord(s.done[i], st));
+  s.pending[i] = true;
+  return TVR_OK;
+}
+
+// Several host arrays packed into ONE upload (one staging buffer, one copy).
+struct UploadBatch {
+  std::vector<char> host;
+  struct Item { size_t host_off; size_t dev_off; size_t bytes; };
+  std::vector<Item> items;
+  template <class T>
+  void add(size_t dev_off, const std::vector<T>& v) {
+    items.push_back({host.size(), dev_off, v.size() * sizeof(T)});
+    const char* p = reinterpret_cast<const char*>(v.data());
+    host.insert(host.end(), p, p + v.size() * sizeof(T));
+  }
+};
+
+int flush_uploads(tvr_model* m, hipStream_t st, char* base, const UploadBatch& ub) {
+  // Items are carved contiguously in order, so the batch is one span.
+  if (ub.items.empty()) return TVR_OK;
+  const size_t first = ub.items.front().dev_off;
+  std::vector<char> span;
+  size_t end = first;
+  for (const auto& it : ub.items) end = std::max(end, it.dev_off + it.bytes);
+  span.assign(end - first, 0);
+  for (const auto& it : ub.items)
+    std::memcpy(span.data() + (it.dev_off - first), ub.host.data() + it.host_off, it.bytes);
+  return upload(m, st, base + first, span.data(), span.size());
+}
+
+hipEvent_t prof_event(tvr_model* m) {
+  hipEvent_t e = nullptr;
+  if (!m->prof_pool.empty()) {
+    e = m->prof_pool.back();
+    m->prof_pool.pop_back();
+  } else if (hipEventCreate(&e) != hipSuccess) {
+    e = nullptr;
+  }
+  return e;
+}
+
+int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M, int N,
+                int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr) {
+  if (M <= 0 || N <= 0) return TVR_OK;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (m && m->prof) {
+    ev0 = prof_event(m);
+    ev1 = prof_event(m);
+    if (ev0) TVR_HIP(hipEventRecord(ev0, st));
+  }
+  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (K=" +
+                                         std::to_string(K) + ")");
+  const dim3 grid(gemm_grid(M, N)), block(GEMM_THREADS);
+  switch (epi) {
+    case EPI_BIAS:
+      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      break;
+    case EPI_SPLIT_GELU:
+      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_SPLIT_GELU>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      break;
+    default:
+      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_RESID>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      break;
+  }
+  TVR_HIP(hipGetLastError());
+  if (ev0 && ev1) {
+    TVR_HIP(hipEventRecord(ev1, st));
+    m->prof_recs.push_back({ev0, ev1, 2.0 * M * N * (double)K,
+                            4.0 * ((double)M * K + (double)N * K + (double)M * N)});
+  }
+  return TVR_OK;
+}
+
+int launch_lnpre(const float* x, int ldx, const int32_t* idx, float* y, int ldy, int rows,
+                 int d, float eps, hipStream_t st) {
+  if (rows <= 0) return TVR_OK;
+  if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
+  const int rows_per_block = 4;
+  hipLaunchKernelGGL(lnpre_kernel, dim3((rows + rows_per_block - 1) / rows_per_block),
+                     dim3(64 * rows_per_block), 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
+// Activation buffers of one launch sequence.
+struct Acts {
+  float* resid;   // [R][d]
+  float* xn;      // [R][d]
+  float* qkv;     // [R][3d]
+  float* a2;      // [R][K2]  (z | gelu(mlp-in))
+};
+
+// One transformer block over the first R rows (Pythia parallel residual):
+//   x = LNPre(resid); [qkv | h] = x @ W1^T + b1; z = attn(qkv); resid += [z|gelu h] @ W2^T + b2
+int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
+              Acts& a, float* qkv_out, const float* cache_qkv, hipStream_t st,
+              const float* z_dst_capture_unused = nullptr) {
+  (void)z_dst_capture_unused;
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model;
+  const tvr_layer_weights& w = m->layers[l];
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, st));
+  GemmEpi e1{};
+  e1.bias = w.b1;
+  e1.out0 = qkv_out;
+  e1.ld0 = 3 * d;
+  e1.out1 = a.a2 + d;
+  e1.ld1 = m->K2;
+  e1.n_split = 3 * d;
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1, d, R, m->D1, d, e1, st, m));
+  if (n_seqs > 0) {
+    const size_t smem = attention_smem_bytes(maxT, c.d_head);
+    if (smem > 64 * 1024)
+      TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(attention_kernel, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st,
+                       qkv_out, 3 * d, cache_qkv, 3 * d, d_seqs, a.a2, m->K2, m->rot_cos,
+                       m->rot_sin, d, c.d_head, c.rotary_dim,
+                       1.0f / std::sqrt((float)c.d_head));
+    TVR_HIP(hipGetLastError());
+  }
+  return TVR_OK;
+}
+
+int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
+  const int d = m->cfg.d_model;
+  const tvr_layer_weights& w = m->layers[l];
+  GemmEpi e2{};
+  e2.bias = w.b2;
+  e2.out0 = a.resid;
+  e2.ld0 = d;
+  e2.resid = a.resid;
+  e2.ldr = d;
+  return launch_gemm(EPI_RESID, a.a2, m->K2, w.w2, m->K2, R, d, m->K2, e2, st, m);
+}
+
+// Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
+int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int32_t* d_targets,
+              int n, float* xf, float* logits_ws, float* out_prob, int32_t* out_topk, int topk,
+              float* out_logits, hipStream_t st) {
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model, V = c.d_vocab;
+  for (int s = 0; s < n; s += kFinalChunk) {
+    const int cn = std::min(kFinalChunk, n - s);
+    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, st));
+    float* lg = out_logits ? out_logits + (size_t)s * V : logits_ws;
+    GemmEpi e{};
+    e.bias = m->b_unembed;
+    e.out0 = lg;
+    e.ld0 = V;
+    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, m->w_unembed_t, d, cn, V, d, e, st, m));
+    hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
+                       d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
+                       out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
+    TVR_HIP(hipGetLastError());
+  }
+  return TVR_OK;
+}
+
+int check_config(const tvr_config& c) {
+  if (c.n_layers <= 0 || c.d_model <= 0 || c.n_heads <= 0 || c.d_head <= 0 || c.d_mlp <= 0 ||
+      c.d_vocab <= 0 || c.n_ctx <= 0)
+    return fail(TVR_ERR_INVALID, "config: all sizes must be positive");
+  if (c.n_heads * c.d_head != c.d_model)
+    return fail(TVR_ERR_INVALID, "config: n_heads * d_head must equal d_model");
+  if (c.rotary_dim < 0 || c.rotary_dim > c.d_head || (c.rotary_dim & 1))
+    return fail(TVR_ERR_INVALID, "config: rotary_dim must be even and <= d_head");
+  if (c.d_model % GEMM_BK != 0 || (c.d_model + c.d_mlp) % GEMM_BK != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "config: d_model and d_model + d_mlp must be multiples of 32");
+  if (c.d_head > 128) return fail(TVR_ERR_UNSUPPORTED, "config: d_head > 128");
+  return TVR_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* tvr_version(void) { return "tvr-mi355x 0.1.0 (gfx950, fp32 MFMA)"; }
+int32_t tvr_abi_version(void) { return TVR_ABI_VERSION; }
+const char* tvr_last_error(void) { return g_last_error.c_str(); }
+
+int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_layer_weights* layers,
+                     const float* w_unembed_t, const float* b_unembed, tvr_model** out) {
+  if (!cfg || !w_embed || !layers || !w_unembed_t || !out)
+    return fail(TVR_ERR_INVALID, "tvr_model_create: null argument");
+  TVR_TRY(check_config(*cfg));
+  for (int l = 0; l < cfg->n_layers; ++l)
+    if (!layers[l].w1 || !layers[l].b1 || !layers[l].w2 || !layers[l].b2)
+      return fail(TVR_ERR_INVALID, "tvr_model_create: null weight in layer " + std::to_string(l));
+  auto* m = new tvr_model();
+  m->cfg = *cfg;
+  m->D1 = 3 * cfg->d_model + cfg->d_mlp;
+  m->K2 = cfg->d_model + cfg->d_mlp;
+  m->w_embed = w_embed;
+  m->layers.assign(layers, layers + cfg->n_layers);
+  m->w_unembed_t = w_unembed_t;
+  m->b_unembed = b_unembed;
+  // TL calculate_sin_cos_rotary: freq = base^(i / (rd/2)), repeated "(2 d)",
+  // angle = pos / freq, all in fp32.
+  const int rd = std::max(cfg->rotary_dim, 2), n_ctx = cfg->n_ctx;
+  std::vector<float> hc((size_t)n_ctx * rd), hs((size_t)n_ctx * rd);
+  const int half = rd / 2;
+  for (int p = 0; p < n_ctx; ++p)
+    for (int i = 0; i < rd; ++i) {
+      const float dim = (float)(i % half);
+      const float freq = std::pow(cfg->rotary_base, dim / (float)half);
+      const float ang = (float)p / freq;
+      hc[(size_t)p * rd + i] = std::cos(ang);
+      hs[(size_t)p * rd + i] = std::sin(ang);
+    }
+  std::vector<const float*> w2s(cfg->n_layers);
+  for (int l = 0; l < cfg->n_layers; ++l) w2s[l] = layers[l].w2;
+  hipError_t e = hipMalloc(&m->rot_cos, hc.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&m->rot_sin, hs.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&m->d_w2s, w2s.size() * sizeof(float*));
+  if (e == hipSuccess) e = hipMemcpy(m->rot_cos, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(m->rot_sin, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(m->d_w2s, w2s.data(), w2s.size() * sizeof(float*), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    tvr_model_destroy(m);
+    return fail(TVR_ERR_HIP, std::string("tvr_model_create: ") + hipGetErrorString(e));
+  }
+  *out = m;
+  return TVR_OK;
+}
+
+int tvr_model_destroy(tvr_model* m) {
+  if (!m) return TVR_OK;
+  (void)hipDeviceSynchronize();
+  if (m->rot_cos) (void)hipFree(m->rot_cos);
+  if (m->rot_sin) (void)hipFree(m->rot_sin);
+  if (m->d_w2s) (void)hipFree(m->d_w2s);
+  if (m->ws) (void)hipFree(m->ws);
+  for (auto& r : m->prof_recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : m->prof_pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) {
+    if (m->staging.buf[i]) (void)hipHostFree(m->staging.buf[i]);
+    if (m->staging.done[i]) (void)hipEventDestroy(m->staging.done[i]);
+  }
+  delete m;
+  return TVR_OK;
+}
+
+size_t tvr_workspace_bytes(const tvr_model* m) { return m ? m->ws_bytes : 0; }
+
+int tvr_profile_enable(tvr_model* m, int32_t on) {
+  if (!m) return fail(TVR_ERR_INVALID, "tvr_profile_enable: null model");
+  TVR_HIP(hipDeviceSynchronize());
+  for (auto& r : m->prof_recs) {
+    m->prof_pool.push_back(r.a);
+    m->prof_pool.push_back(r.b);
+  }
+  m->prof_recs.clear();
+  m->prof = on != 0;
+  return TVR_OK;
+}
+
+int tvr_profile_read(tvr_model* m, tvr_kernel_stats* out) {
+  if (!m || !out) return fail(TVR_ERR_INVALID, "tvr_profile_read: null argument");
+  tvr_kernel_stats s{};
+  for (auto& r : m->prof_recs) {
+    TVR_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    TVR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    s.gemm_launches += 1;
+    s.gemm_flops += r.flops;
+    s.gemm_bytes += r.bytes;
+    s.gemm_ms += ms;
+  }
+  *out = s;
+  return TVR_OK;
+}
+
+int tvr_trace_create(tvr_model* m, int32_t max_seqs, int32_t max_tokens, tvr_trace** out) {
+  if (!m || !out || max_seqs <= 0 || max_tokens <= 0)
+    return fail(TVR_ERR_INVALID, "tvr_trace_create: bad argument");
+  const tvr_config& c = m->cfg;
+  auto* t = new tvr_trace();
+  t->model = m;
+  t->max_seqs = max_seqs;
+  t->max_tokens = max_tokens;
+  const size_t per = (size_t)max_tokens * c.d_model * sizeof(float);
+  hipError_t e = hipMalloc(&t->resid, per * (c.n_layers + 1));
+  if (e == hipSuccess) e = hipMalloc(&t->z, per * c.n_layers);
+  if (e == hipSuccess) e = hipMalloc(&t->qkv, per * 3 * c.n_layers);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    tvr_trace_destroy(t);
+    return fail(TVR_ERR_NOMEM, "tvr_trace_create: device allocation failed");
+  }
+  *out = t;
+  return TVR_OK;
+}
+
+int tvr_trace_destroy(tvr_trace* t) {
+  if (!t) return TVR_OK;
+  (void)hipDeviceSynchronize();
+  if (t->resid) (void)hipFree(t->resid);
+  if (t->z) (void)hipFree(t->z);
+  if (t->qkv) (void)hipFree(t->qkv);
+  delete t;
+  return TVR_OK;
+}
+
+int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, void* stream) {
+  if (!t || !dst) return fail(TVR_ERR_INVALID, "tvr_trace_read: null argument");
+  const int L = t->model->cfg.n_layers, d = t->model->cfg.d_model;
+  const size_t stride = (size_t)t->max_tokens * d;
+  const float* src = nullptr;
+  if (what == TVR_TRACE_RESID_PRE && layer >= 0 && layer <= L) src = t->resid + layer * stride;
+  if (what == TVR_TRACE_Z && layer >= 0 && layer < L) src = t->z + layer * stride;
+  if (!src) return fail(TVR_ERR_INVALID, "tvr_trace_read: bad hook/layer");
+  TVR_HIP(hipMemcpyAsync(dst, src, (size_t)t->n_tokens * d * sizeof(float), hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return TVR_OK;
+}
+
+int32_t tvr_trace_num_tokens(const tvr_trace* t) { return t ? t->n_tokens : 0; }
+
+int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const int32_t* seq_lens,
+                      int32_t n_seq, const int32_t* targets, float* out_prob, int32_t* out_topk,
+                      int32_t topk, float* out_logits, float* capture_zsum, void* stream) {
+  if (!m || !tokens || !seq_lens || n_seq <= 0)
+    return fail(TVR_ERR_INVALID, "tvr_forward_clean: bad argument");
+  if (topk < 0 || topk > STATS_MAX_K) return fail(TVR_ERR_INVALID, "topk must be in [0, 16]");
+  if (topk > 0 && !out_topk) return fail(TVR_ERR_INVALID, "topk > 0 needs out_topk");
+  hipStream_t st = (hipStream_t)stream;
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model, L = c.n_layers;
+  std::vector<int32_t> off(n_seq), last(n_seq);
+  int R = 0, maxT = 0;
+  for (int s = 0; s < n_seq; ++s) {
+    const int T = seq_lens[s];
+    if (T <= 0) return fail(TVR_ERR_INVALID, "sequence " + std::to_string(s) + " is empty");
+    if (T > ATT_MAX_T || T > c.n_ctx)
+      return fail(TVR_ERR_UNSUPPORTED, "sequence length " + std::to_string(T) + " exceeds " +
+                                           std::to_string(std::min(ATT_MAX_T, c.n_ctx)));
+    off[s] = R;
+    last[s] = R + T - 1;
+    R += T;
+    maxT = std::max(maxT, T);
+  }
+  for (int r = 0; r < R; ++r)
+    if (tokens[r] < 0 || tokens[r] >= c.d_vocab)
+      return fail(TVR_ERR_INVALID, "token id " + std::to_string(tokens[r]) + " out of range");
+  if (trace && (n_seq > trace->max_seqs || R > trace->max_tokens))
+    return fail(TVR_ERR_INVALID, "trace capacity exceeded");
+  if (attention_smem_bytes(maxT, c.d_head) > 160 * 1024)
+    return fail(TVR_ERR_UNSUPPORTED, "attention LDS budget exceeded");
+
+  std::vector<SeqDesc> seqs(n_seq);
+  for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1};
+  std::vector<int32_t> tg(n_seq, -1);
+  if (targets) std::copy(targets, targets + n_seq, tg.begin());
+  std::vector<int32_t> tok(tokens, tokens + R);
+
+  const int FC = std::min(kFinalChunk, n_seq);
+  Carve cv;
+  const size_t o_seqs = cv.take<SeqDesc>(n_seq);
+  const size_t o_tok = cv.take<int32_t>(R);
+  const size_t o_last = cv.take<int32_t>(n_seq);
+  const size_t o_tg = cv.take<int32_t>(n_seq);
+  const size_t o_resid = cv.take<float>((size_t)R * d);
+  const size_t o_xn = cv.take<float>((size_t)R * d);
+  const size_t o_qkv = trace ? 0 : cv.take<float>((size_t)R * 3 * d);
+  const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
+  const size_t o_xf = cv.take<float>((size_t)FC * d);
+  const size_t o_lg = out_logits ? 0 : cv.take<float>((size_t)FC * c.d_vocab);
+  const size_t o_cap = capture_zsum ? cv.take<float>((size_t)CAP_GROUPS * d) : 0;
+  TVR_TRY(ensure_workspace(m, cv.off, st));
+  char* base = m->ws;
+  UploadBatch ub;
+  ub.add(o_seqs, seqs);
+  ub.add(o_tok, tok);
+  ub.add(o_last, last);
+  ub.add(o_tg, tg);
+  TVR_TRY(flush_uploads(m, st, base, ub));
+
+  Acts a{(float*)(base + o_resid), (float*)(base + o_xn), trace ? nullptr : (float*)(base + o_qkv),
+         (float*)(base + o_a2)};
+  const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
+  const int32_t* d_last = (const int32_t*)(base + o_last);
+  const size_t tstride = trace ? (size_t)trace->max_tokens * d : 0;
+
+  {
+    const size_t total = (size_t)R * (d / 4);
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(embed_kernel, dim3(blocks), dim3(256), 0, st, (const int32_t*)(base + o_tok),
+                       m->w_embed, a.resid, R, d);
+    TVR_HIP(hipGetLastError());
+  }
+  for (int l = 0; l < L; ++l) {
+    if (trace)
+      TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, (size_t)R * d * sizeof(float),
+                             hipMemcpyDeviceToDevice, st));
+    float* qkv = trace ? trace->qkv + (size_t)l * 3 * tstride : a.qkv;
+    TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, st));
+    if (capture_zsum) {
+      float* part = (float*)(base + o_cap);
+      hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
+                         a.a2, m->K2, d_last, n_seq, part, d);
+      hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part,
+                         capture_zsum + (size_t)l * d, d);
+      TVR_HIP(hipGetLastError());
+    }
+    if (trace)
+      TVR_HIP(hipMemcpy2DAsync(trace->z + l * tstride, d * sizeof(float), a.a2, m->K2 * sizeof(float),
+                               d * sizeof(float), R, hipMemcpyDeviceToDevice, st));
+    TVR_TRY(run_block_out(m, l, R, a, st));
+  }
+  if (trace) {
+    TVR_HIP(hipMemcpyAsync(trace->resid + L * tstride, a.resid, (size_t)R * d * sizeof(float),
+                           hipMemcpyDeviceToDevice, st));
+    trace->seq_off.assign(off.begin(), off.end());
+    trace->seq_len.assign(seq_lens, seq_lens + n_seq);
+    trace->n_seq = n_seq;
+    trace->n_tokens = R;
+  }
+  if (out_prob || out_topk || out_logits)
+    TVR_TRY(run_final(m, a.resid, d_last, (const int32_t*)(base + o_tg), n_seq, (float*)(base + o_xf),
+                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, st));
+  return TVR_OK;
+}
+
+int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites, int32_t n_sites,
+                    const float* vectors, int32_t n_vectors, float* out_prob, int32_t* out_topk,
+                    int32_t topk, float* out_logits, void* stream) {
+  if (!m || !trace || !sites || n_sites <= 0)
+    return fail(TVR_ERR_INVALID, "tvr_patch_sweep: bad argument");
+  if (trace->model != m) return fail(TVR_ERR_INVALID, "trace belongs to another model");
+  if (trace->n_seq <= 0) return fail(TVR_ERR_INVALID, "trace is empty: run tvr_forward_clean first");
+  if (topk < 0 || topk > STATS_MAX_K) return fail(TVR_ERR_INVALID, "topk must be in [0, 16]");
+  if (topk > 0 && !out_topk) return fail(TVR_ERR_INVALID, "topk > 0 needs out_topk");
+  hipStream_t st = (hipStream_t)stream;
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model, L = c.n_layers;
+
+  // --- plan -----------------------------------------------------------------
+  std::vector<int> entry(n_sites), p0(n_sites), nrow(n_sites);
+  int maxT = 0;
+  for (int i = 0; i < n_sites; ++i) {
+    const tvr_site& s = sites[i];
+    if (s.seq < 0 || s.seq >= trace->n_seq)
+      return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": seq out of range");
+    const int T = trace->seq_len[s.seq];
+    maxT = std::max(maxT, T);
+    switch (s.kind) {
+      case TVR_SITE_NONE:
+        entry[i] = L; p0[i] = T - 1; nrow[i] = 1;
+        break;
+      case TVR_SITE_REPLACE_HEAD_ALLPOS:
+        if (s.layer < 0 || s.layer >= L || s.head < 0 || s.head >= c.n_heads)
+          return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": layer/head out of range");
+        if (!vectors || s.vec < 0 || s.vec >= n_vectors)
+          return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": vector out of range");
+        entry[i] = s.layer + 1; p0[i] = 0; nrow[i] = T;
+        break;
+      case TVR_SITE_ADD_ATTN_OUT_LASTPOS:
+        if (s.layer < 0 || s.layer >= L)
+          return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": layer out of range");
+        if (!vectors || s.vec < 0 || s.vec >= n_vectors)
+          return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": vector out of range");
+        entry[i] = s.layer + 1; p0[i] = T - 1; nrow[i] = 1;
+        break;
+      case TVR_SITE_SET_RESID_PRE_POS:
+        if (s.layer < 0 || s.layer >= L || s.pos < 0 || s.pos >= T || s.src_seq < 0 ||
+            s.src_seq >= trace->n_seq || s.src_pos < 0 || s.src_pos >= trace->seq_len[s.src_seq])
+          return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": resid patch out of range");
+        entry[i] = s.layer; p0[i] = s.pos; nrow[i] = T - s.pos;
+        break;
+      default:
+        return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": unknown kind");
+    }
+  }
+  std::vector<int> order(n_sites);
+  for (int i = 0; i < n_sites; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return entry[a] < entry[b]; });
+  std::vector<int> row0(n_sites);
+  std::vector<int> cnt_le(L + 1, 0), rows_le(L + 1, 0);  // sites / rows with entry <= l
+  int R = 0;
+  for (int k = 0; k < n_sites; ++k) {
+    const int i = order[k];
+    row0[i] = R;
+    R += nrow[i];
+  }
+  {
+    int k = 0, rows = 0;
+    for (int l = 0; l <= L; ++l) {
+      while (k < n_sites && entry[order[k]] <= l) { rows += nrow[order[k]]; ++k; }
+      cnt_le[l] = k;
+      rows_le[l] = rows;
+    }
+  }
+  std::vector<SeqDesc> seqs(n_sites);
+  std::vector<EntryDesc> ents(n_sites);
+  for (int k = 0; k < n_sites; ++k) {
+    const int i = order[k];
+    const tvr_site& s = sites[i];
+    const int srow = trace->seq_off[s.seq];
+    seqs[k] = {row0[i], nrow[i], p0[i], srow};
+    EntryDesc e{};
+    e.kind = s.kind;
+    e.row0 = row0[i];
+    e.n = nrow[i];
+    e.p0 = p0[i];
+    e.src_row = srow;
+    e.src2_row = (s.kind == TVR_SITE_SET_RESID_PRE_POS) ? trace->seq_off[s.src_seq] + s.src_pos : 0;
+    e.patch_pos = s.pos;
+    e.head = s.head;
+    e.vec = s.vec;
+    ents[k] = e;
+  }
+  std::vector<int32_t> last(n_sites), tg(n_sites);
+  for (int i = 0; i < n_sites; ++i) {
+    last[i] = row0[i] + nrow[i] - 1;
+    tg[i] = sites[i].target;
+  }
+
+  const int FC = std::min(kFinalChunk, n_sites);
+  Carve cv;
+  const size_t o_seqs = cv.take<SeqDesc>(n_sites);
+  const size_t o_ents = cv.take<EntryDesc>(n_sites);
+  const size_t o_last = cv.take<int32_t>(n_sites);
+  const size_t o_tg = cv.take<int32_t>(n_sites);
+  const size_t o_resid = cv.take<float>((size_t)R * d);
+  const size_t o_xn = cv.take<float>((size_t)R * d);
+  const size_t o_qkv = cv.take<float>((size_t)R * 3 * d);
+  const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
+  const size_t o_xf = cv.take<float>((size_t)FC * d);
+  const size_t o_lg = out_logits ? 0 : cv.take<float>((size_t)FC * c.d_vocab);
+  if (attention_smem_bytes(maxT, c.d_head) > 160 * 1024)
+    return fail(TVR_ERR_UNSUPPORTED, "attention LDS budget exceeded");
+  TVR_TRY(ensure_workspace(m, cv.off, st));
+  char* base = m->ws;
+  UploadBatch ub;
+  ub.add(o_seqs, seqs);
+  ub.add(o_ents, ents);
+  ub.add(o_last, last);
+  ub.add(o_tg, tg);
+  TVR_TRY(flush_uploads(m, st, base, ub));
+
+  Acts a{(float*)(base + o_resid), (float*)(base + o_xn), (float*)(base + o_qkv),
+         (float*)(base + o_a2)};
+  const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
+  const EntryDesc* d_ents = (const EntryDesc*)(base + o_ents);
+  const size_t tstride = (size_t)trace->max_tokens * d;
+
+  auto enter = [&](int l) -> int {
+    const int k0 = l > 0 ? cnt_le[l - 1] : 0, k1 = cnt_le[l];
+    if (k1 <= k0) return TVR_OK;
+    const float* snap = trace->resid + (size_t)l * tstride;
+    const float* zsnap = l > 0 ? trace->z + (size_t)(l - 1) * tstride : nullptr;
+    const float* w2 = l > 0 ? m->layers[l - 1].w2 : nullptr;
+    hipLaunchKernelGGL(entry_kernel, dim3(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS),
+                       dim3(ENTRY_THREADS), 0, st, d_ents + k0, snap, zsnap, w2, m->K2, vectors,
+                       a.resid, d, c.d_head);
+    TVR_HIP(hipGetLastError());
+    return TVR_OK;
+  };
+
+  for (int l = 0; l < L; ++l) {
+    TVR_TRY(enter(l));
+    const int Rl = rows_le[l];
+    if (Rl == 0) continue;
+    TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv,
+                      trace->qkv + (size_t)l * 3 * tstride, st));
+    TVR_TRY(run_block_out(m, l, Rl, a, st));
+  }
+  TVR_TRY(enter(L));
+  return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
+                   (float*)(base + o_xf), out_logits ? nullptr : (float*)(base + o_lg), out_prob,
+                   out_topk, topk, out_logits, st);
+}
+
+int tvr_project_heads(tvr_model* m, const float* zsum, float* out, void* stream) {
+  if (!m || !zsum || !out) return fail(TVR_ERR_INVALID, "tvr_project_heads: null argument");
+  const tvr_config& c = m->cfg;
+  hipLaunchKernelGGL(project_heads_kernel, dim3((c.d_model + 255) / 256, c.n_heads, c.n_layers),
+                     dim3(256), 0, (hipStream_t)stream, zsum, m->d_w2s, m->K2, out, c.n_heads,
+                     c.d_model, c.d_head);
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
+int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw, const float* bias, float* C,
+                 int32_t ldc, int32_t M, int32_t N, int32_t K, void* stream) {
+  if (!A || !W || !C || M < 0 || N < 0 || K <= 0) return fail(TVR_ERR_INVALID, "tvr_gemm_f32: bad argument");
+  GemmEpi e{};
+  e.bias = bias;
+  e.out0 = C;
+  e.ld0 = ldc;
+  return launch_gemm(EPI_BIAS, A, lda, W, ldw, M, N, K, e, (hipStream_t)stream);
+}
+
+int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy, int32_t rows, int32_t d, float eps,
+                  void* stream) {
+  if (!x || !y || rows < 0 || d <= 0) return fail(TVR_ERR_INVALID, "tvr_lnpre_f32: bad argument");
+  return launch_lnpre(x, ldx, nullptr, y, ldy, rows, d, eps, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,392 @@
+// kernels.hpp — the non-GEMM kernels of the patched Pythia forward.
+//
+// All of them are HBM/L2-bound byte movers or tiny contractions; the FLOPs
+// live in gemm_f32.hpp.  Semantics follow TransformerLens as the reference
+// uses it: LayerNormPre after fold_ln, NeoX rotate-half
+// rotary on the first rotary_dim dims, causal softmax in fp32, per-head
+// result = z @ W_O[h] (hook_result, scratch2.py:98,188).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace tvr {
+
+// ---------------------------------------------------------------------------
+// Descriptors built by the host planner (engine.hip).
+
+// One sequence as seen by attention at a layer: its computed rows are the
+// positions [p0, p0+n); positions [0, p0) come from the clean trace's K/V.
+struct SeqDesc {
+  int32_t row0;       // first computed row in the activation buffers
+  int32_t n;          // number of computed rows
+  int32_t p0;         // absolute position of row0
+  int32_t cache_row;  // trace row of position 0 (for the K/V prefix), -1: none
+};
+
+// How a patch site's residual is materialised at its entry layer e
+// (resid_pre[e] rows [p0, p0+n)), from the clean trace.
+struct EntryDesc {
+  int32_t kind;       // tvr_site_kind
+  int32_t row0;       // destination row (activation buffer)
+  int32_t n;          // rows
+  int32_t p0;         // first position
+  int32_t src_row;    // trace row of position 0 of `seq`
+  int32_t src2_row;   // SET_RESID: trace row supplying the patched position
+  int32_t patch_pos;  // SET_RESID: absolute patched position
+  int32_t head;       // REPLACE_HEAD
+  int32_t vec;        // vector row
+  int32_t pad;
+};
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// hook_embed: resid[r] = W_E[tokens[r]]   (one float4 per thread)
+__global__ void embed_kernel(const int32_t* __restrict__ tokens,
+                             const float* __restrict__ W_E, float* __restrict__ out,
+                             int rows, int d) {
+  const int d4 = d >> 2;
+  const size_t total = (size_t)rows * d4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / d4), c = (int)(i % d4);
+    const int tok = tokens[r];
+    ((float4*)out)[i] = ((const float4*)(W_E + (size_t)tok * d))[c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNormPre (TL, after fold_ln): x -= mean(x); x /= sqrt(mean(x^2) + eps).
+// One wave per row; rows optionally gathered through `row_idx`.
+__global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
+                             const int32_t* __restrict__ row_idx,
+                             float* __restrict__ y, int ldy, int rows, int d,
+                             float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (r >= rows) return;
+  const int src = row_idx ? row_idx[r] : r;
+  const float4* xr = (const float4*)(x + (size_t)src * ldx);
+  float4* yr = (float4*)(y + (size_t)r * ldy);
+  const int d4 = d >> 2;
+  float s = 0.f;
+  for (int c = lane; c < d4; c += 64) {
+    const float4 v = xr[c];
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float ss = 0.f;
+  for (int c = lane; c < d4; c += 64) {
+    float4 v = xr[c];
+    v.x -= mean; v.y -= mean; v.z -= mean; v.w -= mean;
+    ss += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+  }
+  const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
+  for (int c = lane; c < d4; c += 64) {
+    float4 v = xr[c];
+    v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;
+    v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
+    yr[c] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Causal attention for ragged sequences with an optional clean K/V prefix.
+// grid = (n_seqs, n_heads), block = 256 (4 waves); each wave owns query rows
+// i = wave, wave+4, ...  K/V of every position live in LDS (rotary applied on
+// load); one score per lane per 64 keys.
+//   qkv  [rows][3d]: q at h*dh, k at d + h*dh, v at 2d + h*dh (pre-rotary)
+//   z    [rows][ldz]: written at h*dh  (attn.hook_z)
+constexpr int ATT_THREADS = 256;
+constexpr int ATT_MAX_T = 128;
+
+__device__ __forceinline__ void rotate_row(float* v, int pos, int rd,
+                                           const float* __restrict__ cos_t,
+                                           const float* __restrict__ sin_t,
+                                           int lane, int nlanes) {
+  // TL apply_rotary (rotate-half / non-adjacent pairs):
+  //   out[i] = x[i]*cos[i] - x[i+rd/2]*sin[i]         i <  rd/2
+  //   out[i] = x[i]*cos[i] + x[i-rd/2]*sin[i]         i >= rd/2
+  const int half = rd >> 1;
+  for (int i = lane; i < half; i += nlanes) {
+    const float x0 = v[i], x1 = v[i + half];
+    const float c0 = cos_t[pos * rd + i], s0 = sin_t[pos * rd + i];
+    const float c1 = cos_t[pos * rd + i + half], s1 = sin_t[pos * rd + i + half];
+    v[i] = x0 * c0 - x1 * s0;
+    v[i + half] = x1 * c1 + x0 * s1;
+  }
+}
+
+__global__ void __launch_bounds__(ATT_THREADS)
+attention_kernel(const float* __restrict__ qkv, int ldq,
+                 const float* __restrict__ cache, int ldc,
+                 const SeqDesc* __restrict__ seqs, float* __restrict__ z, int ldz,
+                 const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                 int d, int dh, int rd, float inv_attn_scale) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const SeqDesc sd = seqs[blockIdx.x];
+  const int h = blockIdx.y;
+  const int T = sd.p0 + sd.n;
+  const int dhp = dh + 1;
+  float* Ks = smem;                    // [T][dh+1]
+  float* Vs = Ks + T * dhp;            // [T][dh+1]
+  float* Qs = Vs + T * dhp;            // [4][dh]
+  float* Ps = Qs + 4 * dh;             // [4][T]
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+
+  // K, V rows: prefix from the clean trace, the rest from this run
+  for (int e = t; e < T * dh; e += ATT_THREADS) {
+    const int j = e / dh, k = e - j * dh;
+    const float* src = (j < sd.p0)
+                           ? cache + (size_t)(sd.cache_row + j) * ldc
+                           : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
+    Ks[j * dhp + k] = src[d + h * dh + k];
+    Vs[j * dhp + k] = src[2 * d + h * dh + k];
+  }
+  __syncthreads();
+  for (int j = wave; j < T; j += 4) rotate_row(Ks + j * dhp, j, rd, cos_t, sin_t, lane, 64);
+  __syncthreads();
+
+  for (int ib = 0; ib < sd.n; ib += 4) {
+    const int i = ib + wave;
+    const bool act = i < sd.n;
+    const int pos = sd.p0 + i;
+    float* q = Qs + wave * dh;
+    float* p = Ps + wave * T;
+    if (act) {
+      const float* qsrc = qkv + (size_t)(sd.row0 + i) * ldq + h * dh;
+      for (int k = lane; k < dh; k += 64) q[k] = qsrc[k];
+    }
+    __syncthreads();
+    if (act) rotate_row(q, pos, rd, cos_t, sin_t, lane, 64);
+    __syncthreads();
+    if (act) {
+      float sc[ATT_MAX_T / 64];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+        const int j = lane + 64 * u;
+        float s = -INFINITY;
+        if (j <= pos && j < T) {
+          const float* kr = Ks + j * dhp;
+          float a = 0.f;
+          for (int k = 0; k < dh; ++k) a += q[k] * kr[k];
+          s = a * inv_attn_scale;
+        }
+        sc[u] = s;
+        mx = fmaxf(mx, s);
+      }
+      mx = wave_max(mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+        const float e = (sc[u] == -INFINITY) ? 0.f : expf(sc[u] - mx);
+        sc[u] = e;
+        sum += e;
+      }
+      sum = wave_sum(sum);
+#pragma unroll
+      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+        const int j = lane + 64 * u;
+        if (j < T) p[j] = sc[u] / sum;
+      }
+    }
+    __syncthreads();
+    if (act) {
+      float* zr = z + (size_t)(sd.row0 + i) * ldz + h * dh;
+      for (int k = lane; k < dh; k += 64) {
+        float a = 0.f;
+        for (int j = 0; j <= pos; ++j) a += p[j] * Vs[j * dhp + k];
+        zr[k] = a;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+inline size_t attention_smem_bytes(int T, int dh) {
+  return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
+}
+
+// ---------------------------------------------------------------------------
+// Site entry: materialise resid_pre[e] rows of every site entering at layer e
+// from the clean trace.  grid = (n_entries, ceil(d/256)); thread owns column c.
+//   snap   trace hook_resid_pre[e]                [tokens][d]
+//   zsnap  trace attn.hook_z[e-1]                 [tokens][d]  (REPLACE_HEAD)
+//   w2     layer e-1 fused [d][d+d_mlp] (cols h*dh.. = W_O[h]^T)
+// REPLACE_HEAD (parallel residual): resid_pre[e] = clean resid_pre[e]
+//   + vec - z[e-1][:, h] @ W_O[e-1, h], at every position (scratch2.py:188).
+constexpr int ENTRY_THREADS = 256;
+constexpr int ENTRY_POS_CHUNK = 8;
+
+__global__ void __launch_bounds__(ENTRY_THREADS)
+entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
+             const float* __restrict__ zsnap, const float* __restrict__ w2, int ldw2,
+             const float* __restrict__ vectors, float* __restrict__ resid, int d, int dh) {
+  const EntryDesc e = ents[blockIdx.x];
+  const int c = blockIdx.y * ENTRY_THREADS + threadIdx.x;
+  if (c >= d) return;
+  if (e.kind == 1) {  // TVR_SITE_REPLACE_HEAD_ALLPOS
+    const float* w = w2 + (size_t)c * ldw2 + e.head * dh;
+    const float vc = vectors[(size_t)e.vec * d + c];
+    for (int p0 = 0; p0 < e.n; p0 += ENTRY_POS_CHUNK) {
+      float acc[ENTRY_POS_CHUNK];
+#pragma unroll
+      for (int u = 0; u < ENTRY_POS_CHUNK; ++u) acc[u] = 0.f;
+      for (int k = 0; k < dh; ++k) {
+        const float wk = w[k];
+#pragma unroll
+        for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
+          const int pos = e.p0 + p0 + u;
+          if (p0 + u < e.n)
+            acc[u] += zsnap[(size_t)(e.src_row + pos) * d + e.head * dh + k] * wk;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
+        if (p0 + u >= e.n) break;
+        const int pos = e.p0 + p0 + u;
+        resid[(size_t)(e.row0 + p0 + u) * d + c] =
+            snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
+      }
+    }
+  } else if (e.kind == 2) {  // TVR_SITE_ADD_ATTN_OUT_LASTPOS
+    for (int i = 0; i < e.n; ++i) {
+      const int pos = e.p0 + i;
+      resid[(size_t)(e.row0 + i) * d + c] =
+          snap[(size_t)(e.src_row + pos) * d + c] + vectors[(size_t)e.vec * d + c];
+    }
+  } else {  // NONE / SET_RESID_PRE_POS: copy rows, one of them from another run
+    for (int i = 0; i < e.n; ++i) {
+      const int pos = e.p0 + i;
+      const int srow = (e.kind == 3 && pos == e.patch_pos) ? e.src2_row : e.src_row + pos;
+      resid[(size_t)(e.row0 + i) * d + c] = snap[(size_t)srow * d + c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Capture + mean-over-prompts reduction, z form (mean_p result =
+// (mean_p z) @ W_O).  Deterministic two-pass: partial[g][c] = sum over rows
+// g, g+G, ...; then zsum[c] += sum_g partial[g][c].
+constexpr int CAP_GROUPS = 64;
+__global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
+                                       const int32_t* __restrict__ rows, int n,
+                                       float* __restrict__ partial, int d) {
+  const int c4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 column
+  const int g = blockIdx.y;
+  if (c4 * 4 >= d) return;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = g; i < n; i += CAP_GROUPS) {
+    const float4 v = ((const float4*)(z + (size_t)rows[i] * ldz))[c4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  ((float4*)(partial + (size_t)g * d))[c4] = s;
+}
+__global__ void capture_finish_kernel(const float* __restrict__ partial,
+                                      float* __restrict__ zsum, int d) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f;
+  for (int g = 0; g < CAP_GROUPS; ++g) s += partial[(size_t)g * d + c];
+  zsum[c] += s;
+}
+
+// out[l][h][c] = sum_k zsum[l][h*dh + k] * w2_l[c][h*dh + k]
+__global__ void project_heads_kernel(const float* __restrict__ zsum,
+                                     const float* const* __restrict__ w2s, int ldw2,
+                                     float* __restrict__ out, int H, int d, int dh) {
+  const int l = blockIdx.z, h = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d) return;
+  const float* w = w2s[l] + (size_t)c * ldw2 + h * dh;
+  const float* zz = zsum + (size_t)l * d + h * dh;
+  float a = 0.f;
+  for (int k = 0; k < dh; ++k) a += zz[k] * w[k];
+  out[((size_t)l * H + h) * d + c] = a;
+}
+
+// ---------------------------------------------------------------------------
+// Last-row statistics: softmax(logits)[target], top-k ids (descending value,
+// lowest id first on ties: torch.argmax's first-occurrence rule).
+constexpr int STATS_THREADS = 256;
+constexpr int STATS_MAX_K = 16;
+
+__global__ void __launch_bounds__(STATS_THREADS)
+row_stats_kernel(const float* __restrict__ logits, int ldl, int V,
+                 const int32_t* __restrict__ targets, float* __restrict__ out_prob,
+                 int32_t* __restrict__ out_topk, int topk) {
+  __shared__ float s_val[STATS_THREADS / 64];
+  __shared__ int s_idx[STATS_THREADS / 64];
+  __shared__ float s_red[STATS_THREADS / 64];
+  __shared__ int s_sel[STATS_MAX_K];
+  const int r = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const float* x = logits + (size_t)r * ldl;
+
+  // block max
+  float mx = -INFINITY;
+  for (int v = t; v < V; v += STATS_THREADS) mx = fmaxf(mx, x[v]);
+  mx = wave_max(mx);
+  if (lane == 0) s_red[wave] = mx;
+  __syncthreads();
+  mx = s_red[0];
+  for (int w = 1; w < STATS_THREADS / 64; ++w) mx = fmaxf(mx, s_red[w]);
+  __syncthreads();
+  // sum of exp
+  float se = 0.f;
+  for (int v = t; v < V; v += STATS_THREADS) se += expf(x[v] - mx);
+  se = wave_sum(se);
+  if (lane == 0) s_red[wave] = se;
+  __syncthreads();
+  if (t == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < STATS_THREADS / 64; ++w) tot += s_red[w];
+    if (out_prob) {
+      const int tg = targets ? targets[r] : -1;
+      out_prob[r] = (tg >= 0 && tg < V) ? expf(x[tg] - mx) / tot : 0.f;
+    }
+  }
+  if (!out_topk || topk <= 0) return;
+  // top-k: k rounds of (value desc, index asc) block argmax with exclusion
+  for (int j = 0; j < topk; ++j) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = t; v < V; v += STATS_THREADS) {
+      bool taken = false;
+      for (int q = 0; q < j; ++q) taken |= (s_sel[q] == v);
+      if (taken) continue;
+      const float xv = x[v];
+      if (xv > bv || (xv == bv && v < bi)) { bv = xv; bi = v; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { s_val[wave] = bv; s_idx[wave] = bi; }
+    __syncthreads();
+    if (t == 0) {
+      float fv = s_val[0];
+      int fi = s_idx[0];
+      for (int w = 1; w < STATS_THREADS / 64; ++w)
+        if (s_val[w] > fv || (s_val[w] == fv && s_idx[w] < fi)) { fv = s_val[w]; fi = s_idx[w]; }
+      s_sel[j] = fi;
+      out_topk[(size_t)r * topk + j] = fi;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace tvr

@@ -1,0 +1,324 @@
+"""The reference's experiment entry points, same names and signatures,
+executed as batched sweeps on the HIP engine.
+
+Each function replaces a Python loop of batch-1 TransformerLens forwards
+(one per prompt x patch site) with one clean-forward launch sequence and one
+patch-sweep launch sequence whose batch enumerates the sites:
+
+  generate_mean_activation                     scratch2.py:81-100   (a1)
+  gather_head_activations_to_layers            scratch2.py:103-104  (a2)
+  apply_layered_vectors_to_zero_shot           scratch2.py:114-127  (a3, a4)
+  apply_layered_vectors_to_zero_shot_by_probability  scratch2.py:135-150 (a5)
+  calculate_average_causal_indirect_effect     scratch2.py:171-197  (a6, a7)
+  assemble_task_vector                         scratch2.py:232-238  (a10)
+  logits_to_next_k_tokens, check_accuracy_of_task_vector,
+  check_accuracy_of_added_task_vector          scratch2.py:278-314  (a11)
+  test_component_hypothesis                    scratch.py:106-147   (a12)
+  substitute_task                              scratch.py:164-213
+
+Drop-in notes
+* ``model`` is an ``amd.Model`` instead of a HookedTransformer; it must be
+  passed (the reference's defaults bind a module-global model).
+* Late-binding closure (App. B1): the reference's layer sweeps add
+  ``layered_vectors[-1]`` at every layer.  ``reference_late_binding=True``
+  (default) reproduces that; ``False`` adds ``layered_vectors[i]`` at layer i.
+* Accuracy compares decoded strings exactly as the reference (B5).
+* ``assemble_task_vector`` accepts device tensors (the reference's
+  ``.numpy()`` needs CPU tensors, B9).
+"""
+from __future__ import annotations
+
+import random
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .model import Model, make_sites
+from .prompts import (Pairs, assemble_end_list_tasks, construct_query, generate_shuffled_prompt,  # noqa: F401
+                      generate_shuffled_prompts, icl_multi_token, icl_single_token, sample_icl_prompts)
+
+# Sites per patch_sweep launch (bounds the activation workspace: a CIE site
+# of a T-token prompt holds T rows).
+MAX_SITES_PER_LAUNCH = 16384
+# Prompts per clean-forward launch during extraction.
+EXTRACT_BATCH = 2048
+
+
+def _chunks(n: int, size: int):
+    for s in range(0, n, size):
+        yield s, min(n, s + size)
+
+
+# ------------------------------------------------------------------ a1 / a2
+def generate_mean_activation(contexts: Pairs, function_token: str, seperator_token: str = ",",
+                             model: Model = None, num_contexts: int = 1024, len_contexts: int = 4
+                             ) -> torch.Tensor:
+    """Mean over ``num_contexts`` ICL prompts of ``blocks.{l}.attn.hook_result``
+    at the last position, for every layer and head: [n_layers, n_heads, d_model].
+    Captured in z form on the GPU and projected once (mean is linear)."""
+    prompts = sample_icl_prompts(model, contexts, function_token, seperator_token, num_contexts,
+                                 len_contexts)
+    return model.project_heads(sum_last_z(model, prompts)) / num_contexts
+
+
+def sum_last_z(model: Model, prompts: Sequence[Sequence[int]]) -> torch.Tensor:
+    """Σ over prompts of hook_z at the last position, [L, d] (fp32, device)."""
+    total = None
+    for a, b in _chunks(len(prompts), EXTRACT_BATCH):
+        z = model.forward_clean(prompts[a:b], capture=True)["zsum"]
+        total = z if total is None else total + z
+    return total
+
+
+def gather_head_activations_to_layers(mean_head_activations: torch.Tensor) -> torch.Tensor:
+    return mean_head_activations.sum(1)
+
+
+# ------------------------------------------------------------- a3 / a4 / a5
+def _layer_vectors(layered_vectors: torch.Tensor, model: Model, late_binding: bool):
+    v = layered_vectors.to(model.device, torch.float32)
+    if late_binding:
+        return v[-1:].contiguous(), lambda layer: 0
+    if v.shape[0] != model.cfg.n_layers:
+        raise ValueError("layered_vectors must have one row per layer")
+    return v.contiguous(), lambda layer: layer
+
+
+def _injection_sweep(model: Model, seqs: List[List[int]], vectors: torch.Tensor, vec_of_layer,
+                     layers: Sequence[int], targets: Optional[List[int]], topk: int):
+    """Clean forward of ``seqs`` + one ADD_ATTN_OUT_LASTPOS site per
+    (prompt, layer).  Returns (clean outputs, patched outputs [n, len(layers)])."""
+    n = len(seqs)
+    trace = model.trace(n, sum(len(s) for s in seqs))
+    clean = model.forward_clean(seqs, targets=targets, topk=topk, trace=trace)
+    sites = make_sites(n * len(layers))
+    sites["seq"] = np.repeat(np.arange(n), len(layers))
+    sites["layer"] = np.tile(np.asarray(layers), n)
+    sites["kind"] = _lib.SITE_ADD_ATTN_OUT_LASTPOS
+    sites["vec"] = [vec_of_layer(l) for l in sites["layer"]]
+    if targets is not None:
+        sites["target"] = np.repeat(np.asarray(targets), len(layers))
+    patched = {}
+    for a, b in _chunks(len(sites), MAX_SITES_PER_LAUNCH):
+        out = model.patch_sweep(trace, sites[a:b], vectors, topk=topk, want_prob=targets is not None)
+        for k, v in out.items():
+            patched.setdefault(k, []).append(v)
+    patched = {k: torch.cat(v).view(n, len(layers), *v[0].shape[1:]) for k, v in patched.items()}
+    return clean, patched
+
+
+def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: Pairs, function_token: str,
+                                       model: Model = None, reference_late_binding: bool = True) -> List[float]:
+    """Per-layer top-1 accuracy of zero-shot ``[BOS, x, f]`` prompts with a
+    vector added to ``hook_attn_out[0, -1]`` at that layer."""
+    L = model.cfg.n_layers
+    vectors, vec_of = _layer_vectors(layered_vectors, model, reference_late_binding)
+    f = model.to_single_token(function_token)
+    seqs = [[0, model.to_single_token(x), f] for x, _ in contexts]
+    _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, topk=1)
+    top1 = patched["topk"][..., 0].cpu().tolist()
+    hits = [0] * L
+    for (x, y), row in zip(contexts, top1):
+        for i, tid in enumerate(row):
+            hits[i] += model.to_string(tid) == y
+    return [1.0 * h / len(contexts) for h in hits]
+
+
+def apply_layered_vectors_to_zero_shot_by_probability(layered_vectors: torch.Tensor, contexts: Pairs,
+                                                      function_token: str, model: Model = None,
+                                                      reference_late_binding: bool = True) -> torch.Tensor:
+    """Per-layer mean change of the first answer token's probability
+    (patched − clean), [n_layers] on the device."""
+    L = model.cfg.n_layers
+    vectors, vec_of = _layer_vectors(layered_vectors, model, reference_late_binding)
+    f = model.to_single_token(function_token)
+    enc = model.tokenizer.encode
+    seqs = [[0] + enc(x) + [f] for x, _ in contexts]
+    targets = [enc(y)[0] for _, y in contexts]
+    clean, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), targets, topk=0)
+    return (patched["prob"] - clean["prob"][:, None]).sum(0) / len(contexts)
+
+
+# ------------------------------------------------------------------- a6 / a7
+def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Sequence[Sequence[int]],
+                                answers: Sequence[int], model: Model,
+                                layers: Optional[Sequence[int]] = None,
+                                heads: Optional[Sequence[int]] = None) -> torch.Tensor:
+    """Σ over prompts of p_patched(answer) − p_clean(answer) for every
+    (layer, head) site, [n_layers, n_heads] (zeros outside ``layers``/``heads``).
+    ``prompts`` are token ids (BOS included); one clean forward + one
+    staircase sweep per launch-sized group of prompts."""
+    cfg = model.cfg
+    L, H = cfg.n_layers, cfg.n_heads
+    layers = list(range(L)) if layers is None else list(layers)
+    heads = list(range(H)) if heads is None else list(heads)
+    grid_l = np.repeat(np.asarray(layers, dtype=np.int32), len(heads))
+    grid_h = np.tile(np.asarray(heads, dtype=np.int32), len(layers))
+    per_prompt = grid_l.size
+    vectors = mean_head_activations.to(model.device, torch.float32).reshape(L * H, cfg.d_model).contiguous()
+    out = torch.zeros(L, H, device=model.device)
+    group = max(1, MAX_SITES_PER_LAUNCH // max(per_prompt, 1))
+    for a, b in _chunks(len(prompts), group):
+        seqs = [list(map(int, p)) for p in prompts[a:b]]
+        tg = [int(t) for t in answers[a:b]]
+        n = len(seqs)
+        trace = model.trace(n, sum(len(s) for s in seqs))
+        p0 = model.forward_clean(seqs, targets=tg, trace=trace)["prob"]
+        sites = make_sites(n * per_prompt)
+        sites["seq"] = np.repeat(np.arange(n, dtype=np.int32), per_prompt)
+        sites["kind"] = _lib.SITE_REPLACE_HEAD_ALLPOS
+        sites["layer"] = np.tile(grid_l, n)
+        sites["head"] = np.tile(grid_h, n)
+        sites["vec"] = sites["layer"] * H + sites["head"]
+        sites["target"] = np.repeat(np.asarray(tg, dtype=np.int32), per_prompt)
+        p = model.patch_sweep(trace, sites, vectors)["prob"].view(n, per_prompt)
+        delta = (p - p0[:, None]).sum(0)
+        out.index_put_((torch.as_tensor(grid_l, device=model.device).long(),
+                        torch.as_tensor(grid_h, device=model.device).long()), delta, accumulate=True)
+    return out
+
+
+def calculate_average_causal_indirect_effect(mean_head_activations: torch.Tensor, scrambled_prompts,
+                                             prompt_answers, model: Model = None) -> torch.Tensor:
+    """CIE[l, h] = mean over prompts of softmax(patched)[answer[0]] −
+    softmax(clean)[answer[0]], where the patch writes ``mean[l, h]`` into
+    ``hook_result[0, :, h]`` at every position.  [n_layers, n_heads]."""
+    cfg = model.cfg
+    if tuple(mean_head_activations.shape) != (cfg.n_layers, cfg.n_heads, cfg.d_model):
+        raise ValueError("Mean head activations must be of shape (n_layers, n_heads, d_model)")
+    if len(scrambled_prompts) != len(prompt_answers):
+        raise ValueError("Prompt answers must be of the same length as scrambled prompts")
+    prompts = [model.to_tokens(p)[0].tolist() if isinstance(p, str) else list(p) for p in scrambled_prompts]
+    answers = [a[0] if isinstance(a, (list, tuple)) else int(a) for a in prompt_answers]
+    return causal_indirect_effect_sums(mean_head_activations, prompts, answers, model) / len(prompts)
+
+
+# ---------------------------------------------------------------- a10 / a11
+def assemble_task_vector(mean_head_activations: torch.Tensor, causal_indirect_effects: torch.Tensor,
+                         layer: int, num_heads: int) -> torch.Tensor:
+    """Sum of the mean outputs of the ``num_heads`` highest-CIE heads in
+    layers ≤ ``layer`` (torch.topk order and tie rule, as the reference)."""
+    sub = causal_indirect_effects[: layer + 1, :]
+    _, idx = torch.topk(sub.flatten(), num_heads)
+    H = sub.shape[1]
+    rows = mean_head_activations[(idx // H).to(mean_head_activations.device),
+                                 (idx % H).to(mean_head_activations.device)]
+    vec = torch.zeros(mean_head_activations.shape[-1], dtype=mean_head_activations.dtype,
+                      device=mean_head_activations.device)
+    for r in rows:  # sequential adds, the reference's summation order
+        vec += r
+    return vec
+
+
+def logits_to_next_k_tokens(k: int, logits: torch.Tensor, model: Model = None) -> List[str]:
+    return [model.to_string(e) for e in torch.topk(logits[0, -1, :], k).indices.tolist()]
+
+
+def _fv_topk(task_vector, layer: int, contexts: Pairs, topk: int, model: Model, with_baseline: bool):
+    seqs = [model.to_tokens(x + ":")[0].tolist() for x, _ in contexts]
+    firsts = [model.to_string(model.tokenizer.encode(y)[0]) for _, y in contexts]
+    vec = task_vector.to(model.device, torch.float32).reshape(1, -1).contiguous()
+    clean, patched = _injection_sweep(model, seqs, vec, lambda l: 0, [layer], None, topk=topk)
+    def hits(top):
+        return sum(first in [model.to_string(t) for t in row] for first, row in zip(firsts, top.tolist()))
+    fv = hits(patched["topk"][:, 0].cpu())
+    base = hits(clean["topk"].cpu()) if with_baseline else None
+    return base, fv
+
+
+def check_accuracy_of_task_vector(task_vector: torch.Tensor, layer: int, contexts: Pairs, topk: int = 5,
+                                  model: Model = None) -> Tuple[float, float]:
+    """(zero-shot top-k accuracy, top-k accuracy with the FV added to
+    ``hook_attn_out[0, -1]`` at ``layer``) for prompts ``x + ":"``."""
+    base, fv = _fv_topk(task_vector, layer, contexts, topk, model, True)
+    return (1.0 * base / len(contexts), 1.0 * fv / len(contexts))
+
+
+def check_accuracy_of_added_task_vector(task_vector: torch.Tensor, layer: int, contexts: Pairs, topk: int = 5,
+                                        model: Model = None) -> float:
+    _, fv = _fv_topk(task_vector, layer, contexts, topk, model, False)
+    return 1.0 * fv / len(contexts)
+
+
+# ---------------------------------------------------------------------- a12
+def test_component_hypothesis(contexts: Pairs, function_token: str, model: Model = None,
+                              num_contexts: int = 256, len_contexts: int = 4, batch_contexts: int = 512):
+    """Layer sweep of residual patching: the ICL run's ``hook_resid_pre[L][-2]``
+    written into a dummy-query run, continued from layer L.  Returns
+    (total, baseline hits, regular hits, [hits per layer])."""
+    L = model.cfg.n_layers
+    pool = list(contexts)
+    draws = []
+    for _ in range(num_contexts):
+        random.shuffle(pool)
+        demos, query = pool[:len_contexts], pool[len_contexts]
+        draws.append((demos, query, pool[len_contexts + 1][0]))
+    base_hits = normal_hits = 0
+    per_layer = [0] * L
+    for a, b in _chunks(len(draws), batch_contexts):
+        seqs, answers = [], []
+        for demos, query, dummy in draws[a:b]:
+            seqs.append(model.to_tokens(construct_query(query, function_token)[0])[0].tolist())
+            seqs.append(icl_single_token(model, demos, query[0], function_token, None))
+            seqs.append(icl_single_token(model, demos, dummy, function_token, None))
+            answers.append(query[1])
+        n = len(answers)
+        trace = model.trace(3 * n, sum(len(s) for s in seqs))
+        top = model.forward_clean(seqs, topk=1, trace=trace)["topk"][:, 0].cpu().view(n, 3).tolist()
+        sites = make_sites(n * L)
+        T = np.asarray([len(seqs[3 * i + 2]) for i in range(n)], dtype=np.int32)
+        sites["kind"] = _lib.SITE_SET_RESID_PRE_POS
+        sites["seq"] = np.repeat(3 * np.arange(n) + 2, L)
+        sites["src_seq"] = np.repeat(3 * np.arange(n) + 1, L)
+        sites["pos"] = np.repeat(T - 2, L)
+        sites["src_pos"] = np.repeat(T - 2, L)
+        sites["layer"] = np.tile(np.arange(L), n)
+        pt = model.patch_sweep(trace, sites, None, topk=1, want_prob=False)["topk"][:, 0].cpu().view(n, L).tolist()
+        for i, ans in enumerate(answers):
+            base_hits += model.to_string(top[i][0]) == ans
+            normal_hits += model.to_string(top[i][1]) == ans
+            for l in range(L):
+                per_layer[l] += model.to_string(pt[i][l]) == ans
+    return (num_contexts, base_hits, normal_hits, per_layer)
+
+
+def substitute_task(taskA: Pairs, taskB: Pairs, layer: int, function_token: str = "→", model: Model = None,
+                    num_contexts: int = 256, len_contexts: int = 4):
+    """Swap ``hook_resid_pre[layer][-1]`` between a task-A and a task-B run of
+    the same query.  Returns (n, A hits, B hits, A←B hits on B's answer,
+    B←A hits on A's answer).  Sorts both task lists in place (App. B6)."""
+    if len(taskA) != len(taskB):
+        raise ValueError("The two tasks must have the same length")
+    taskA.sort(key=lambda p: p[0])
+    taskB.sort(key=lambda p: p[0])
+    if any(a[0] != b[0] for a, b in zip(taskA, taskB)):
+        raise ValueError("The two tasks must have the same domains")
+    mixed = [(a[0], a[1], b[1]) for a, b in zip(taskA, taskB)]
+    seqs, ans = [], []
+    for _ in range(num_contexts):
+        random.shuffle(mixed)
+        ctx_a = [(m[0], m[1]) for m in mixed[:len_contexts]]
+        ctx_b = [(m[0], m[2]) for m in mixed[:len_contexts]]
+        q = mixed[len_contexts][0][0]  # first character of the query item, as scratch.py:189
+        seqs.append(icl_single_token(model, ctx_a, q, function_token, None))
+        seqs.append(icl_single_token(model, ctx_b, q, function_token, None))
+        ans.append((mixed[len_contexts][1], mixed[len_contexts][2]))
+    n = num_contexts
+    trace = model.trace(2 * n, sum(len(s) for s in seqs))
+    top = model.forward_clean(seqs, topk=1, trace=trace)["topk"][:, 0].cpu().view(n, 2).tolist()
+    sites = make_sites(2 * n)
+    T = np.asarray([len(s) for s in seqs], dtype=np.int32)
+    sites["kind"] = _lib.SITE_SET_RESID_PRE_POS
+    sites["layer"] = layer
+    sites["seq"] = np.arange(2 * n)
+    sites["src_seq"] = np.arange(2 * n) ^ 1  # A takes B's row, B takes A's
+    sites["pos"] = T - 1
+    sites["src_pos"] = T[np.arange(2 * n) ^ 1] - 1
+    pt = model.patch_sweep(trace, sites, None, topk=1, want_prob=False)["topk"][:, 0].cpu().view(n, 2).tolist()
+    a_hits = sum(model.to_string(top[i][0]) == ans[i][0] for i in range(n))
+    b_hits = sum(model.to_string(top[i][1]) == ans[i][1] for i in range(n))
+    a_to_b = sum(model.to_string(pt[i][0]) == ans[i][1] for i in range(n))
+    b_to_a = sum(model.to_string(pt[i][1]) == ans[i][0] for i in range(n))
+    return (num_contexts, a_hits, b_hits, a_to_b, b_to_a)

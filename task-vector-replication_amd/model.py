@@ -1,0 +1,265 @@
+"""``Model``: the handle the façade passes where the reference passes a
+TransformerLens ``HookedTransformer`` (scratch2.py:26 and every ``model=``
+argument).  It owns the processed device weights, exposes ``cfg`` and the
+token helpers, and drives the engine's batched entry points:
+
+* ``forward_clean``  — many prompts in one launch sequence (replaces the
+  per-prompt ``forward`` / ``run_with_cache`` calls);
+* ``patch_sweep``    — many (prompt, patch site) pairs in one staircase
+  launch sequence (replaces the per-site ``run_with_hooks`` loops);
+* ``project_heads``  — z-form capture → ``hook_result`` form.
+
+All device work is enqueued on torch's current stream; nothing here has a
+CPU fallback (the engine refuses to run without a GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import CConfig, PythiaConfig, get_config
+from .tokenizer import HFTokenizer, SyntheticTokenizer, TokenizerMixin
+from .weights import EngineWeights, load_hf_safetensors, process_to_engine, synth_engine_weights
+
+SITE_DTYPE = np.dtype([(f, np.int32) for f in _lib.SITE_FIELDS])
+
+
+def make_sites(n: int) -> np.ndarray:
+    """Zeroed site records (layout of ``tvr_site``), target = -1."""
+    s = np.zeros(n, dtype=SITE_DTYPE)
+    s["target"] = -1
+    return s
+
+
+class Trace:
+    """Engine-owned clean-run snapshots (resid_pre per layer, z, K/V)."""
+
+    def __init__(self, model: "Model", max_seqs: int, max_tokens: int):
+        self._lib = model._lib
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.tvr_trace_create(model._h, max_seqs, max_tokens, ctypes.byref(h)),
+                   "tvr_trace_create")
+        self._h = h
+        self.model = model
+        self.max_seqs = max_seqs
+        self.max_tokens = max_tokens
+        self.seq_lens: List[int] = []
+        self.seq_offsets: List[int] = []
+
+    def resid_pre(self, layer: int) -> torch.Tensor:
+        """``blocks.{layer}.hook_resid_pre`` of every traced token ([tokens, d]);
+        layer == n_layers gives the final residual."""
+        return self._read(_lib.TRACE_RESID_PRE, layer)
+
+    def z(self, layer: int) -> torch.Tensor:
+        """``blocks.{layer}.attn.hook_z`` flattened over heads ([tokens, d])."""
+        return self._read(_lib.TRACE_Z, layer)
+
+    def _read(self, what: int, layer: int) -> torch.Tensor:
+        m = self.model
+        buf = torch.empty(sum(self.seq_lens), m.cfg.d_model, device=m.device)
+        _lib.check(self._lib.tvr_trace_read(self._h, what, layer, buf.data_ptr(), m._stream()),
+                   "tvr_trace_read")
+        return buf
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.tvr_trace_destroy(h)
+            self._h = None
+
+
+class Model(TokenizerMixin):
+    def __init__(self, cfg: PythiaConfig, weights: EngineWeights, tokenizer=None,
+                 device: Optional[torch.device] = None):
+        self._h = None
+        self._lib = _lib.load()
+        dev = torch.device(device) if device is not None else weights.w_embed.device
+        if dev.type != "cuda" or not torch.cuda.is_available():
+            raise _lib.EngineError("the HIP engine needs a GPU device (no CPU fallback): "
+                                   f"got device {dev}")
+        self.cfg = cfg
+        self.device = dev
+        self.weights = weights
+        self.tokenizer = tokenizer if tokenizer is not None else SyntheticTokenizer(cfg.d_vocab)
+        for t in weights.tensors():
+            if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("engine weights must be contiguous fp32 tensors on the model device")
+        self._cfg_c = CConfig.from_config(cfg)
+        self._layers_c = (_lib.CLayerWeights * cfg.n_layers)(
+            *[_lib.CLayerWeights(L.w1.data_ptr(), L.b1.data_ptr(), L.w2.data_ptr(), L.b2.data_ptr())
+              for L in weights.layers])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            _lib.check(self._lib.tvr_model_create(
+                ctypes.byref(self._cfg_c), weights.w_embed.data_ptr(), self._layers_c,
+                weights.w_unembed_t.data_ptr(), weights.b_unembed.data_ptr(), ctypes.byref(h)),
+                "tvr_model_create")
+        self._h = h
+        self._trace_cache: Optional[Trace] = None
+
+    # ------------------------------------------------------------------ build
+    @classmethod
+    def from_pretrained(cls, name: str, device="cuda", seed: int = 0, checkpoint: Optional[str] = None,
+                        tokenizer_path: Optional[str] = None, std: float = 0.02, ln_std: float = 0.1,
+                        cfg: Optional[PythiaConfig] = None) -> "Model":
+        """``HookedTransformer.from_pretrained`` without a network: the named
+        Pythia shape with seeded synthetic weights (generated on the device), or
+        a local HF-layout safetensors ``checkpoint``."""
+        cfg = cfg if cfg is not None else get_config(name)
+        dev = torch.device(device)
+        if checkpoint:
+            w = process_to_engine(cfg, load_hf_safetensors(checkpoint), device=dev, free_source=True)
+        else:
+            w = synth_engine_weights(cfg, seed=seed, device=dev, std=std, ln_std=ln_std)
+        tok = HFTokenizer(tokenizer_path) if tokenizer_path else None
+        return cls(cfg, w, tokenizer=tok, device=dev)
+
+    @classmethod
+    def from_hf_state_dict(cls, cfg: PythiaConfig, sd, device="cuda", tokenizer=None) -> "Model":
+        return cls(cfg, process_to_engine(cfg, sd, device=torch.device(device)), tokenizer, device)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._trace_cache = None
+            self._lib.tvr_model_destroy(h)
+            self._h = None
+
+    # ------------------------------------------------------------- internals
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def trace(self, n_seqs: int, n_tokens: int) -> Trace:
+        """A trace with at least this capacity (reused across calls)."""
+        t = self._trace_cache
+        if t is None or t.max_seqs < n_seqs or t.max_tokens < n_tokens:
+            self._trace_cache = None
+            t = Trace(self, max(n_seqs, 1), max(n_tokens, 1))
+            self._trace_cache = t
+        return t
+
+    @staticmethod
+    def _pack(seqs: Sequence[Sequence[int]]):
+        lens = np.asarray([len(s) for s in seqs], dtype=np.int32)
+        toks = np.asarray([int(x) for s in seqs for x in s], dtype=np.int32)
+        return toks, lens
+
+    # ---------------------------------------------------------- entry points
+    def forward_clean(self, seqs: Sequence[Sequence[int]], targets: Optional[Sequence[int]] = None,
+                      topk: int = 0, return_logits: bool = False, capture: bool = False,
+                      trace: Optional[Trace] = None) -> Dict[str, torch.Tensor]:
+        """Batched clean forward of ragged prompts (token-id lists).
+        Returns ``prob`` [n] (softmax(logits[-1])[target]), ``topk`` [n, k],
+        ``logits`` [n, V] (last position), ``zsum`` [L, d] (sum over prompts of
+        hook_z at the last position) as requested."""
+        n = len(seqs)
+        if n == 0:
+            raise ValueError("no prompts")
+        toks, lens = self._pack(seqs)
+        tg = None
+        if targets is not None:
+            tg = np.asarray([-1 if t is None else int(t) for t in targets], dtype=np.int32)
+            if tg.shape[0] != n:
+                raise ValueError("targets must have one entry per prompt")
+        dev = self.device
+        out = {}
+        prob = torch.empty(n, device=dev) if tg is not None else None
+        top = torch.empty(n, topk, dtype=torch.int32, device=dev) if topk else None
+        logits = torch.empty(n, self.cfg.d_vocab, device=dev) if return_logits else None
+        zsum = torch.zeros(self.cfg.n_layers, self.cfg.d_model, device=dev) if capture else None
+        if trace is not None and (trace.max_seqs < n or trace.max_tokens < int(lens.sum())):
+            raise ValueError("trace too small for this batch")
+        rc = self._lib.tvr_forward_clean(
+            self._h, trace._h if trace is not None else None,
+            toks.ctypes.data, lens.ctypes.data, n,
+            tg.ctypes.data if tg is not None else None,
+            _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits), _lib.ptr(zsum), self._stream())
+        _lib.check(rc, "tvr_forward_clean")
+        if trace is not None:
+            trace.seq_lens = lens.tolist()
+            trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
+        if prob is not None:
+            out["prob"] = prob
+        if top is not None:
+            out["topk"] = top
+        if logits is not None:
+            out["logits"] = logits
+        if zsum is not None:
+            out["zsum"] = zsum
+        return out
+
+    def patch_sweep(self, trace: Trace, sites: np.ndarray, vectors: Optional[torch.Tensor] = None,
+                    topk: int = 0, want_prob: bool = True, return_logits: bool = False
+                    ) -> Dict[str, torch.Tensor]:
+        """Evaluate every site (records of ``make_sites``) against ``trace``."""
+        sites = np.ascontiguousarray(sites, dtype=SITE_DTYPE)
+        n = int(sites.shape[0])
+        if n == 0:
+            raise ValueError("no patch sites")
+        nvec = 0
+        if vectors is not None:
+            if vectors.device != self.device or vectors.dtype != torch.float32:
+                raise ValueError("vectors must be fp32 on the model device")
+            vectors = vectors.reshape(-1, self.cfg.d_model).contiguous()
+            nvec = vectors.shape[0]
+        dev = self.device
+        prob = torch.empty(n, device=dev) if want_prob else None
+        top = torch.empty(n, topk, dtype=torch.int32, device=dev) if topk else None
+        logits = torch.empty(n, self.cfg.d_vocab, device=dev) if return_logits else None
+        rc = self._lib.tvr_patch_sweep(self._h, trace._h, sites.ctypes.data, n, _lib.ptr(vectors), nvec,
+                                       _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits),
+                                       self._stream())
+        _lib.check(rc, "tvr_patch_sweep")
+        out = {}
+        if prob is not None:
+            out["prob"] = prob
+        if top is not None:
+            out["topk"] = top
+        if logits is not None:
+            out["logits"] = logits
+        return out
+
+    def project_heads(self, zsum: torch.Tensor) -> torch.Tensor:
+        """[L, d] z-sums → [L, H, d] hook_result sums."""
+        zsum = zsum.contiguous()
+        out = torch.empty(self.cfg.n_layers, self.cfg.n_heads, self.cfg.d_model, device=self.device)
+        _lib.check(self._lib.tvr_project_heads(self._h, zsum.data_ptr(), out.data_ptr(), self._stream()),
+                   "tvr_project_heads")
+        return out
+
+    # ------------------------------------------------------------ profiling
+    def profile(self, on: bool) -> None:
+        """Enable/disable HIP-event timing of every GEMM launch (resets totals)."""
+        _lib.check(self._lib.tvr_profile_enable(self._h, 1 if on else 0), "tvr_profile_enable")
+
+    def profile_stats(self) -> dict:
+        st = _lib.CKernelStats()
+        _lib.check(self._lib.tvr_profile_read(self._h, ctypes.byref(st)), "tvr_profile_read")
+        return {"gemm_launches": st.gemm_launches, "gemm_flops": st.gemm_flops, "gemm_ms": st.gemm_ms,
+                "gemm_bytes": st.gemm_bytes}
+
+    # ------------------------------------------------- TL-style conveniences
+    def _as_ids(self, tokens) -> List[int]:
+        if isinstance(tokens, str):
+            tokens = self.to_tokens(tokens)
+        if isinstance(tokens, torch.Tensor):
+            if tokens.dim() == 2:
+                if tokens.shape[0] != 1:
+                    raise ValueError("batch size must be 1")
+                tokens = tokens[0]
+            return [int(x) for x in tokens.tolist()]
+        return [int(x) for x in tokens]
+
+    def forward(self, tokens) -> torch.Tensor:
+        """Logits of the LAST position, shaped [1, 1, V] (the reference only
+        ever reads ``logits[0, -1]``: scratch2.py:43,112,144,184,192,280)."""
+        out = self.forward_clean([self._as_ids(tokens)], return_logits=True)
+        return out["logits"].view(1, 1, -1)
+
+    __call__ = forward

@@ -1,0 +1,202 @@
+"""Weights: seeded synthetic Pythia checkpoints and TransformerLens processing.
+
+``HookedTransformer.from_pretrained`` (scratch.py:26, scratch2.py:26) fetches a
+checkpoint by name and, with its defaults, processes it with ``fold_ln``,
+``center_writing_weights``, ``center_unembed`` and ``fold_value_biases``.  Those
+steps define the numerical value of every hook the reference reads
+(``hook_result`` excludes b_O and the folded value bias; residuals and logits
+are mean-centred), so the engine applies the same processing once at load and
+lays the result out for its fused GEMMs:
+
+* ``w1`` [3d + d_mlp, d]: Q | K | V | MLP-in rows (LN1/LN2 folded, read-in
+  weights centred over d_model).  LN1 and LN2 both read ``resid_pre`` in a
+  parallel block and are identical LayerNormPre after folding, so one
+  normalisation feeds one GEMM.
+* ``w2`` [d, d + d_mlp]: O | MLP-out columns (write-out weights centred).
+* ``b2`` = b_O (+ folded value bias) + b_out.
+
+No network: weights are either generated from a seed (shapes of a named
+Pythia) or loaded from a local HF-layout safetensors file.
+"""
+from __future__ import annotations
+
+import zlib
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from .config import PythiaConfig
+
+HFStateDict = Dict[str, torch.Tensor]
+
+
+def _seed_for(seed: int, name: str) -> int:
+    return (int(seed) * 0x9E3779B1 + zlib.crc32(name.encode())) & 0x7FFF_FFFF_FFFF
+
+
+def hf_param_shapes(cfg: PythiaConfig) -> Dict[str, tuple]:
+    """Parameter names/shapes of ``transformers.GPTNeoXForCausalLM``."""
+    d, m, V = cfg.d_model, cfg.d_mlp, cfg.d_vocab
+    shapes = {"gpt_neox.embed_in.weight": (V, d)}
+    for l in range(cfg.n_layers):
+        p = f"gpt_neox.layers.{l}."
+        shapes.update({
+            p + "input_layernorm.weight": (d,),
+            p + "input_layernorm.bias": (d,),
+            p + "post_attention_layernorm.weight": (d,),
+            p + "post_attention_layernorm.bias": (d,),
+            p + "attention.query_key_value.weight": (3 * d, d),
+            p + "attention.query_key_value.bias": (3 * d,),
+            p + "attention.dense.weight": (d, d),
+            p + "attention.dense.bias": (d,),
+            p + "mlp.dense_h_to_4h.weight": (m, d),
+            p + "mlp.dense_h_to_4h.bias": (m,),
+            p + "mlp.dense_4h_to_h.weight": (d, m),
+            p + "mlp.dense_4h_to_h.bias": (d,),
+        })
+    shapes["gpt_neox.final_layer_norm.weight"] = (d,)
+    shapes["gpt_neox.final_layer_norm.bias"] = (d,)
+    shapes["embed_out.weight"] = (V, d)
+    return shapes
+
+
+def synth_param(cfg: PythiaConfig, name: str, shape: tuple, seed: int = 0,
+                device="cpu", std: float = 0.02, ln_std: float = 0.1) -> torch.Tensor:
+    """One seeded synthetic parameter (SURVEY.md §8d value distributions):
+    weights N(0, std), LayerNorm weights 1 + N(0, ln_std), biases N(0, std)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(_seed_for(seed, name))
+    x = torch.randn(shape, generator=g, device=device, dtype=torch.float32)
+    if "layernorm" in name or "layer_norm" in name:
+        return (1.0 + ln_std * x) if name.endswith("weight") else x.mul_(std)
+    return x.mul_(std)
+
+
+def synth_hf_state_dict(cfg: PythiaConfig, seed: int = 0, device="cpu", std: float = 0.02,
+                        ln_std: float = 0.1) -> HFStateDict:
+    """A full seeded synthetic HF-layout state dict (biases and LN params
+    non-trivial so fold_ln / fold_value_biases are exercised)."""
+    return {n: synth_param(cfg, n, s, seed, device, std, ln_std)
+            for n, s in hf_param_shapes(cfg).items()}
+
+
+def load_hf_safetensors(path: str, device="cpu") -> HFStateDict:
+    """Load a local HF GPT-NeoX checkpoint (safetensors, no code execution)."""
+    from safetensors.torch import load_file
+    sd = load_file(path, device=str(device))
+    return {k: v.float() for k, v in sd.items()}
+
+
+@dataclass
+class EngineLayer:
+    w1: torch.Tensor
+    b1: torch.Tensor
+    w2: torch.Tensor
+    b2: torch.Tensor
+
+
+@dataclass
+class EngineWeights:
+    """Processed weights in the engine layout (all fp32, contiguous)."""
+    w_embed: torch.Tensor          # [V, d]
+    layers: List[EngineLayer]
+    w_unembed_t: torch.Tensor      # [V, d]  (TL W_U transposed)
+    b_unembed: torch.Tensor        # [V]
+
+    def tensors(self) -> List[torch.Tensor]:
+        out = [self.w_embed, self.w_unembed_t, self.b_unembed]
+        for L in self.layers:
+            out += [L.w1, L.b1, L.w2, L.b2]
+        return out
+
+
+def _process_layer(cfg: PythiaConfig, get) -> EngineLayer:
+    d, H, dh = cfg.d_model, cfg.n_heads, cfg.d_head
+    ln1_w, ln1_b = get("input_layernorm.weight"), get("input_layernorm.bias")
+    ln2_w, ln2_b = get("post_attention_layernorm.weight"), get("post_attention_layernorm.bias")
+    # HF fuses Q, K, V per head: rows (head, {q,k,v}, d_head).  Engine order: Q | K | V,
+    # each (head, d_head).
+    wqkv = get("attention.query_key_value.weight").view(H, 3, dh, d).transpose(0, 1).reshape(3 * d, d)
+    bqkv = get("attention.query_key_value.bias").view(H, 3, dh).transpose(0, 1).reshape(3 * d)
+    w_in, b_in = get("mlp.dense_h_to_4h.weight"), get("mlp.dense_h_to_4h.bias")
+    # fold_ln: biases first (they read the unscaled weights), then scale, then centre
+    # the read-in weights over d_model.
+    bqkv = bqkv + wqkv @ ln1_b
+    b_in = b_in + w_in @ ln2_b
+    wqkv = wqkv * ln1_w
+    w_in = w_in * ln2_w
+    wqkv = wqkv - wqkv.mean(dim=1, keepdim=True)
+    w_in = w_in - w_in.mean(dim=1, keepdim=True)
+    # center_writing_weights: W_O, b_O, W_out, b_out centred over the d_model output.
+    w_o, b_o = get("attention.dense.weight"), get("attention.dense.bias")
+    w_out, b_out = get("mlp.dense_4h_to_h.weight"), get("mlp.dense_4h_to_h.bias")
+    w_o = w_o - w_o.mean(dim=0, keepdim=True)
+    w_out = w_out - w_out.mean(dim=0, keepdim=True)
+    b_o = b_o - b_o.mean()
+    b_out = b_out - b_out.mean()
+    # fold_value_biases: b_O += sum_h b_V[h] @ W_O[h]; b_V = 0.
+    b_v = bqkv[2 * d:].clone()
+    b_o = b_o + w_o @ b_v
+    bqkv = torch.cat([bqkv[: 2 * d], torch.zeros_like(b_v)])
+    return EngineLayer(
+        w1=torch.cat([wqkv, w_in], 0).contiguous(),
+        b1=torch.cat([bqkv, b_in]).contiguous(),
+        w2=torch.cat([w_o, w_out], 1).contiguous(),
+        b2=(b_o + b_out).contiguous(),
+    )
+
+
+def _process_unembed(w_u: torch.Tensor, lnf_w: torch.Tensor, lnf_b: torch.Tensor):
+    """ln_final folded into W_U (HF embed_out.weight [V, d] = TL W_U^T), then
+    center_unembed.  Pythia has no unembed bias, so b_U starts at 0."""
+    b_u = w_u @ lnf_b
+    w_u = w_u * lnf_w
+    w_u = w_u - w_u.mean(dim=1, keepdim=True)            # fold_ln centring over d_model
+    w_u = w_u - w_u.mean(dim=0, keepdim=True)            # center_unembed over vocab
+    b_u = b_u - b_u.mean()
+    return w_u.contiguous(), b_u.contiguous()
+
+
+@torch.no_grad()
+def process_to_engine(cfg: PythiaConfig, sd: HFStateDict, device=None,
+                      free_source: bool = False, dtype=torch.float32) -> EngineWeights:
+    """TransformerLens ``process_weights_`` (fold_ln → center_writing_weights →
+    center_unembed → fold_value_biases) straight into the engine layout.
+    ``free_source`` pops tensors from ``sd`` as it goes (bounds peak memory)."""
+    dev = device if device is not None else sd["gpt_neox.embed_in.weight"].device
+
+    def take(name):
+        t = sd.pop(name) if free_source else sd[name]
+        return t.to(dev, dtype)
+
+    w_e = take("gpt_neox.embed_in.weight")
+    w_e = (w_e - w_e.mean(dim=1, keepdim=True)).contiguous()
+    layers = []
+    for l in range(cfg.n_layers):
+        p = f"gpt_neox.layers.{l}."
+        layers.append(_process_layer(cfg, lambda n, p=p: take(p + n)))
+    w_u, b_u = _process_unembed(take("embed_out.weight"), take("gpt_neox.final_layer_norm.weight"),
+                                take("gpt_neox.final_layer_norm.bias"))
+    return EngineWeights(w_e, layers, w_u, b_u)
+
+
+@torch.no_grad()
+def synth_engine_weights(cfg: PythiaConfig, seed: int = 0, device="cpu", std: float = 0.02,
+                         ln_std: float = 0.1) -> EngineWeights:
+    """Generate + process layer by layer (peak memory ~1 layer of raw weights),
+    the path used for the multi-GB configs on the GPU."""
+    shapes = hf_param_shapes(cfg)
+
+    def gen(name):
+        return synth_param(cfg, name, shapes[name], seed, device, std, ln_std)
+
+    w_e = gen("gpt_neox.embed_in.weight")
+    w_e = (w_e - w_e.mean(dim=1, keepdim=True)).contiguous()
+    layers = []
+    for l in range(cfg.n_layers):
+        p = f"gpt_neox.layers.{l}."
+        layers.append(_process_layer(cfg, lambda n, p=p: gen(p + n)))
+    w_u, b_u = _process_unembed(gen("embed_out.weight"), gen("gpt_neox.final_layer_norm.weight"),
+                                gen("gpt_neox.final_layer_norm.bias"))
+    return EngineWeights(w_e, layers, w_u, b_u)

@@ -1,0 +1,61 @@
+"""CPU: the C-ABI library builds, loads, and exports every symbol that
+include/tvr.h declares (no compute calls without a GPU)."""
+import ctypes
+import re
+from pathlib import Path
+
+import tvr_amd
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_functions():
+    text = (ROOT / "include" / "tvr.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tvr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_entry_points():
+    names = declared_functions()
+    for want in ("tvr_model_create", "tvr_forward_clean", "tvr_patch_sweep", "tvr_project_heads",
+                 "tvr_trace_create", "tvr_trace_read", "tvr_gemm_f32"):
+        assert want in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(str(tvr_amd._lib.LIB_PATH))
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert set(declared_functions()) == set(tvr_amd._lib.SIGNATURES)
+
+
+def test_version_and_errors_without_gpu():
+    lib = tvr_amd._lib.load()
+    assert lib.tvr_abi_version() == 1
+    assert b"gfx950" in lib.tvr_version()
+    # argument validation runs before any device call
+    out = ctypes.c_void_p()
+    rc = lib.tvr_model_create(None, None, None, None, None, ctypes.byref(out))
+    assert rc == tvr_amd._lib.TVR_ERR_INVALID
+    assert b"null" in lib.tvr_last_error()
+
+
+def test_site_record_layout_matches_header():
+    text = (ROOT / "include" / "tvr.h").read_text()
+    body = re.search(r"typedef struct tvr_site \{(.*?)\} tvr_site;", text, re.S).group(1)
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert fields == tvr_amd._lib.SITE_FIELDS
+    assert tvr_amd.model.SITE_DTYPE.itemsize == 4 * len(fields)
+
+
+def test_model_refuses_cpu_device(tiny_cfg):
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    w = tvr_amd.weights.synth_engine_weights(tiny_cfg, seed=0)
+    with pytest.raises(tvr_amd._lib.EngineError, match="no CPU fallback"):
+        tvr_amd.Model(tiny_cfg, w)

@@ -1,0 +1,283 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Tolerances (fp32 engine vs fp32 oracle; the GEMM reduction order differs):
+* logits / residuals / z: |Δ| ≤ 1e-4 · max|ref| (typically ~1e-6)
+* extracted mean vectors: ≤ 1e-4 relative (north-star bar)
+* probabilities: |Δp| ≤ 1e-5 · max p, CIE: |Δ| ≤ 1e-4 · max|CIE| + 1e-7
+* top-1 / top-k ids and string accuracies: identical (near-ties excluded
+  where the fp64 oracle's gap is below 1e-5)
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import tvr_amd
+from oracle import reference_experiments as R
+
+pytestmark = pytest.mark.gpu
+
+ARROW = tvr_amd.tasks.ARROW
+
+
+def rel_err(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+# ------------------------------------------------------------------ kernels
+@pytest.mark.parametrize("M,N,K", [(1, 1, 32), (37, 130, 64), (128, 128, 32), (300, 257, 320),
+                                   (1000, 2560, 2560), (129, 50304, 64)])
+def test_gemm_f32_matches_torch(M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g)
+    b = torch.randn(N, generator=g)
+    C = torch.empty(M, N, device="cuda")
+    lib = tvr_amd._lib.load()
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    tvr_amd._lib.check(lib.tvr_gemm_f32(Ad.data_ptr(), K, Wd.data_ptr(), K, bd.data_ptr(), C.data_ptr(), N,
+                                        M, N, K, torch.cuda.current_stream().cuda_stream), "gemm")
+    ref = A.double() @ W.double().T + b.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    bound = 4e-7 * (A.double().abs() @ W.double().abs().T).max().item() + 1e-6
+    assert err <= bound, (err, bound)
+    # fp32 torch reference of the same op, as a sanity anchor
+    t32 = (Ad @ Wd.T + bd).cpu().double()
+    assert (t32 - ref).abs().max().item() <= 2 * bound
+
+
+def test_lnpre_matches_torch():
+    x = torch.randn(77, 2560, device="cuda") * 3 + 1
+    y = torch.empty_like(x)
+    lib = tvr_amd._lib.load()
+    tvr_amd._lib.check(lib.tvr_lnpre_f32(x.data_ptr(), 2560, y.data_ptr(), 2560, 77, 2560, 1e-5,
+                                         torch.cuda.current_stream().cuda_stream), "lnpre")
+    xd = x.double()
+    xd = xd - xd.mean(-1, keepdim=True)
+    ref = xd / (xd.pow(2).mean(-1, keepdim=True) + 1e-5).sqrt()
+    assert (y.double() - ref).abs().max().item() < 2e-6
+
+
+# ------------------------------------------------------------ clean forward
+def ragged_prompts(n, vocab, seed, lo=2, hi=40):
+    rng = random.Random(seed)
+    return [[0] + [rng.randrange(1, vocab) for _ in range(rng.randrange(lo, hi))] for _ in range(n)]
+
+
+def test_forward_clean_matches_oracle(tiny_model, tiny_oracle):
+    prompts = ragged_prompts(9, tiny_model.cfg.d_vocab, 1) + [[0], [0, 5], list(range(128))]
+    targets = [p[-1] for p in prompts]
+    out = tiny_model.forward_clean(prompts, targets=targets, topk=5, return_logits=True)
+    for i, p in enumerate(prompts):
+        ref = tiny_oracle.forward(torch.tensor([p]))[0, -1]
+        assert rel_err(out["logits"][i], ref) < 1e-4, i
+        pr = torch.softmax(ref, 0)
+        assert abs(out["prob"][i].item() - pr[targets[i]].item()) <= 1e-5 * pr.max().item()
+        assert out["topk"][i].tolist() == torch.topk(ref, 5).indices.tolist()
+
+
+def test_trace_matches_run_with_cache(tiny_model, tiny_oracle):
+    prompts = ragged_prompts(5, tiny_model.cfg.d_vocab, 2)
+    trace = tiny_model.trace(len(prompts), sum(map(len, prompts)))
+    tiny_model.forward_clean(prompts, trace=trace)
+    off = 0
+    L = tiny_model.cfg.n_layers
+    resid = [trace.resid_pre(l).cpu() for l in range(L + 1)]
+    zs = [trace.z(l).cpu() for l in range(L)]
+    for p in prompts:
+        _, cache = tiny_oracle.run_with_cache(torch.tensor([p]))
+        T = len(p)
+        for l in range(L):
+            assert rel_err(resid[l][off:off + T], cache[f"blocks.{l}.hook_resid_pre"][0]) < 1e-4
+            assert rel_err(zs[l][off:off + T], cache[f"blocks.{l}.attn.hook_z"][0].reshape(T, -1)) < 1e-4
+        assert rel_err(resid[L][off:off + T], cache[f"blocks.{L - 1}.hook_resid_post"][0]) < 1e-4
+        off += T
+
+
+def test_forward_rejects_bad_input(tiny_model):
+    with pytest.raises(ValueError):
+        tiny_model.forward_clean([[0, 1], []])
+    with pytest.raises(ValueError):
+        tiny_model.forward_clean([[0, tiny_model.cfg.d_vocab]])
+    with pytest.raises(RuntimeError):
+        tiny_model.forward_clean([[0] * 129])
+
+
+# --------------------------------------------------------------- experiments
+@pytest.fixture(scope="module")
+def mean_pair(tiny_model, tiny_oracle):
+    random.seed(1234)
+    ours = tvr_amd.generate_mean_activation(tvr_amd.tasks.letter_to_caps, ARROW, ",", model=tiny_model,
+                                            num_contexts=96, len_contexts=4)
+    random.seed(1234)
+    ref = R.generate_mean_activation(tvr_amd.tasks.letter_to_caps, ARROW, ",", model=tiny_oracle,
+                                     num_contexts=96, len_contexts=4)
+    return ours, ref
+
+
+def test_generate_mean_activation(mean_pair):
+    ours, ref = mean_pair
+    assert ours.shape == ref.shape
+    assert rel_err(ours, ref) < 1e-4
+
+
+def test_layer_sweeps_late_binding(tiny_model, tiny_oracle, mean_pair):
+    ours_mean, ref_mean = mean_pair
+    ctx = tvr_amd.tasks.letter_to_caps
+    lv_ours = tvr_amd.gather_head_activations_to_layers(ours_mean)
+    lv_ref = R.gather_head_activations_to_layers(ref_mean)
+    acc = tvr_amd.apply_layered_vectors_to_zero_shot(lv_ours * 8, ctx, ARROW, model=tiny_model)
+    acc_ref = R.apply_layered_vectors_to_zero_shot(lv_ref * 8, ctx, ARROW, tiny_oracle)
+    assert acc == acc_ref
+    dp = tvr_amd.apply_layered_vectors_to_zero_shot_by_probability(lv_ours * 8, ctx, ARROW, model=tiny_model)
+    dp_ref = R.apply_layered_vectors_to_zero_shot_by_probability(lv_ref * 8, ctx, ARROW, tiny_oracle)
+    assert (dp.cpu().double() - dp_ref.double()).abs().max().item() <= 1e-4 * dp_ref.abs().max().item() + 1e-7
+
+
+def test_layer_sweep_per_layer_vectors(tiny_model, tiny_oracle, mean_pair):
+    """Intended per-layer semantics (no closure quirk) = the reference hooks
+    with one vector per layer."""
+    ours_mean, ref_mean = mean_pair
+    ctx = tvr_amd.tasks.fruit_to_color
+    lv = tvr_amd.gather_head_activations_to_layers(ours_mean) * 8
+    acc = tvr_amd.apply_layered_vectors_to_zero_shot(lv, ctx, ARROW, model=tiny_model,
+                                                     reference_late_binding=False)
+    lv_ref = R.gather_head_activations_to_layers(ref_mean) * 8
+    hits = [0] * tiny_oracle.cfg.n_layers
+    for x, y in ctx:
+        tokens = torch.tensor([0, tiny_oracle.to_single_token(x), tiny_oracle.to_single_token(ARROW)])
+        for i in range(tiny_oracle.cfg.n_layers):
+            logits = tiny_oracle.run_with_hooks(tokens, fwd_hooks=[
+                (f"blocks.{i}.hook_attn_out", lambda hv, hook, v=lv_ref[i]: R.layer_addition_hook(hv, hook, v))])
+            hits[i] += R.logits_to_next_token(logits, tiny_oracle) == y
+    assert acc == [h / len(ctx) for h in hits]
+
+
+def test_causal_indirect_effect(tiny_model, tiny_oracle, mean_pair):
+    ours_mean, ref_mean = mean_pair
+    random.seed(99)
+    prompts, answers = tvr_amd.generate_shuffled_prompts(tvr_amd.tasks.letter_to_caps, tiny_model, 6, 4, ARROW)
+    random.seed(99)
+    prompts_r, answers_r = R.generate_shuffled_prompts(tvr_amd.tasks.letter_to_caps, tiny_oracle, 6, 4, ARROW)
+    assert prompts == prompts_r and answers == answers_r
+    cie = tvr_amd.calculate_average_causal_indirect_effect(ours_mean, prompts, answers, model=tiny_model)
+    cie_ref = R.calculate_average_causal_indirect_effect(ref_mean, prompts_r, answers_r, tiny_oracle)
+    assert cie.shape == cie_ref.shape
+    assert (cie.cpu().double() - cie_ref.double()).abs().max().item() <= 1e-4 * cie_ref.abs().max().item() + 1e-7
+    # function vector from the top heads, then its zero-shot top-5 accuracy
+    fv = tvr_amd.assemble_task_vector(ours_mean, cie, 1, 3)
+    fv_ref = R.assemble_task_vector(ref_mean, cie_ref, 1, 3)
+    assert rel_err(fv, fv_ref) < 1e-4
+    ctx = tvr_amd.tasks.letter_to_caps[:40]
+    acc = tvr_amd.check_accuracy_of_task_vector(fv * 4, 1, ctx, model=tiny_model)
+    acc_ref = R.check_accuracy_of_task_vector(fv_ref * 4, 1, ctx, model=tiny_oracle)
+    assert acc == acc_ref
+    assert tvr_amd.check_accuracy_of_added_task_vector(fv * 4, 0, ctx, model=tiny_model) == \
+        R.check_accuracy_of_added_task_vector(fv_ref * 4, 0, ctx, model=tiny_oracle)
+
+
+def test_cie_validation(tiny_model):
+    with pytest.raises(ValueError, match="Mean head activations"):
+        tvr_amd.calculate_average_causal_indirect_effect(torch.zeros(1, 2, 3, device="cuda"), ["a"], [[1]],
+                                                         model=tiny_model)
+    cfg = tiny_model.cfg
+    with pytest.raises(ValueError, match="same length"):
+        tvr_amd.calculate_average_causal_indirect_effect(
+            torch.zeros(cfg.n_layers, cfg.n_heads, cfg.d_model, device="cuda"), ["a", "b"], [[1]], model=tiny_model)
+
+
+def test_component_hypothesis(tiny_model, tiny_oracle):
+    random.seed(5)
+    ours = tvr_amd.test_component_hypothesis(tvr_amd.tasks.low_to_caps, ARROW, model=tiny_model, num_contexts=40,
+                                             len_contexts=4, batch_contexts=16)
+    random.seed(5)
+    ref = R.test_component_hypothesis(tvr_amd.tasks.low_to_caps, ARROW, model=tiny_oracle, num_contexts=40,
+                                      len_contexts=4)
+    assert ours == ref
+
+
+def test_substitute_task(tiny_model, tiny_oracle):
+    random.seed(6)
+    ours = tvr_amd.substitute_task(list(tvr_amd.tasks.letter_to_caps), list(tvr_amd.tasks.letter_to_low), 1,
+                                   ARROW, model=tiny_model, num_contexts=32, len_contexts=4)
+    random.seed(6)
+    ref = R.substitute_task(list(tvr_amd.tasks.letter_to_caps), list(tvr_amd.tasks.letter_to_low), 1, ARROW,
+                            model=tiny_oracle, num_contexts=32, len_contexts=4)
+    assert ours == ref
+
+
+def test_patch_sweep_site_kinds_against_hooks(tiny_model, tiny_oracle):
+    """Every site kind on ragged prompts, compared with the oracle's hook on
+    the same prompt (logits of the last position)."""
+    cfg = tiny_model.cfg
+    prompts = ragged_prompts(4, cfg.d_vocab, 11, lo=3, hi=30)
+    trace = tiny_model.trace(4, sum(map(len, prompts)))
+    tiny_model.forward_clean(prompts, trace=trace)
+    g = torch.Generator().manual_seed(3)
+    vecs = torch.randn(5, cfg.d_model, generator=g)
+    sites = tvr_amd.make_sites(4 * 4)
+    want = []
+    k = 0
+    for i, p in enumerate(prompts):
+        T = len(p)
+        for kind in range(4):
+            s = sites[k]
+            s["seq"], s["kind"], s["target"] = i, kind, p[1]
+            tokens = torch.tensor([p])
+            if kind == 0:
+                ref = tiny_oracle.forward(tokens)
+            elif kind == 1:
+                l, h = (i + 1) % cfg.n_layers, i % cfg.n_heads
+                s["layer"], s["head"], s["vec"] = l, h, i
+                tiny_oracle.cfg.use_attn_result = True
+                def hook(hv, hook, h=h, v=vecs[i]):
+                    hv[0, :, h, :] = v
+                    return hv
+                ref = tiny_oracle.run_with_hooks(tokens, fwd_hooks=[(f"blocks.{l}.attn.hook_result", hook)])
+                tiny_oracle.cfg.use_attn_result = False
+            elif kind == 2:
+                l = i % cfg.n_layers
+                s["layer"], s["vec"] = l, 4
+                ref = tiny_oracle.run_with_hooks(tokens, fwd_hooks=[
+                    (f"blocks.{l}.hook_attn_out", lambda hv, hook: R.layer_addition_hook(hv, hook, vecs[4]))])
+            else:
+                l, src = i % cfg.n_layers, (i + 1) % len(prompts)
+                pos, spos = T // 2, len(prompts[src]) // 3
+                s["layer"], s["pos"], s["src_seq"], s["src_pos"] = l, pos, src, spos
+                _, c_dst = tiny_oracle.run_with_cache(tokens)
+                _, c_src = tiny_oracle.run_with_cache(torch.tensor([prompts[src]]))
+                r = c_dst[f"blocks.{l}.hook_resid_pre"].clone()
+                r[0, pos] = c_src[f"blocks.{l}.hook_resid_pre"][0, spos]
+                ref = tiny_oracle.forward(r, start_at_layer=l)
+            want.append(ref[0, -1])
+            k += 1
+    out = tiny_model.patch_sweep(trace, sites, vecs.cuda(), topk=3, return_logits=True)
+    for j, ref in enumerate(want):
+        assert rel_err(out["logits"][j], ref) < 1e-4, (j, sites[j])
+        assert out["topk"][j].tolist() == torch.topk(ref, 3).indices.tolist(), j
+        pr = torch.softmax(ref, 0)[int(sites[j]["target"])].item()
+        assert abs(out["prob"][j].item() - pr) <= 1e-5 * torch.softmax(ref, 0).max().item()
+
+
+@pytest.mark.slow
+def test_pythia160m_shape_cie_subset(tokenizer):
+    """Pythia-160m shape (d 768, 12 heads, d_head 64): clean logits and a CIE
+    stripe (3 layers x 12 heads, 2 prompts) against the fp32 oracle."""
+    from conftest import make_oracle
+    cfg = tvr_amd.get_config("pythia-160m")
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda")
+    oracle = make_oracle(cfg, sd, model.tokenizer)
+    prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, 2, 4, seed=1234)
+    g = torch.Generator().manual_seed(0)
+    mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5
+    layers = [0, 6, 11]
+    ours = tvr_amd.experiments.causal_indirect_effect_sums(mean.cuda(), prompts, answers, model, layers=layers)
+    ref = R.calculate_average_causal_indirect_effect(mean, prompts, [[a] for a in answers], oracle,
+                                                     layers=layers) * len(prompts)
+    assert (ours.cpu().double() - ref.double()).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-9
+    out = model.forward_clean(prompts, return_logits=True)
+    for i, p in enumerate(prompts):
+        assert rel_err(out["logits"][i], oracle.forward(torch.tensor([p]))[0, -1]) < 1e-4
