@@ -83,6 +83,8 @@ class Model(TokenizerMixin):
         if dev.type != "cuda" or not torch.cuda.is_available():
             raise _lib.EngineError("the HIP engine needs a GPU device (no CPU fallback): "
                                    f"got device {dev}")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
         self.cfg = cfg
         self.device = dev
         self.weights = weights
