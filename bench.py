@@ -43,11 +43,25 @@ def parse():
     ap.add_argument("--model", default="pythia-2.8b")
     ap.add_argument("--prompts", type=int, default=12, help="CIE prompts per GPU per step")
     ap.add_argument("--kshot", type=int, default=4)
-    ap.add_argument("--extract", type=int, default=256, help="prompts for the (untimed) mean extraction")
+    ap.add_argument("--extract", type=int, default=0,
+                    help="prompts for an (untimed) mean extraction; 0 = seeded random mean vectors, so every GEMM "
+                         "launch of the process belongs to a CIE step (rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
     return ap.parse_args()
+
+
+def pmc_traffic():
+    """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary of
+    this bench command (profiles/pmc_gemm_latest.json, written by
+    tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE passes with
+    the gfx950 x2 FETCH_SIZE correction).  None if absent."""
+    p = ROOT / "profiles" / "pmc_gemm_latest.json"
+    if not p.exists():
+        return None, None
+    d = json.loads(p.read_text())
+    return d.get("hbm_bytes_per_launch"), f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
 
 
 def log(*a):
@@ -102,17 +116,23 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] {args.model} synthetic weights on {dev} in {time.time() - t0:.1f}s")
 
-    # --- mean head activations (a1), untimed: synthetic 6-shot prompts (T=28)
-    import random
-    random.seed(4321)
-    pairs = tvr_amd.tasks.synthetic_task(52, cfg.d_vocab, seed=7)
-    ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, pairs, "→", ",", args.extract, 6)
-    torch.cuda.synchronize()
-    te = time.perf_counter()
-    zsum = sum_last_z(model, ex_prompts)
-    torch.cuda.synchronize()
-    te = time.perf_counter() - te
-    mean = model.project_heads(zsum) / len(ex_prompts)
+    # --- mean head activations [L, H, d]: a real extraction (a1) or seeded random
+    te, n_ex = None, 0
+    if args.extract > 0:
+        import random
+        random.seed(4321)
+        pairs = tvr_amd.tasks.synthetic_task(52, cfg.d_vocab, seed=7)
+        ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, pairs, "→", ",", args.extract, 6)
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        zsum = sum_last_z(model, ex_prompts)
+        torch.cuda.synchronize()
+        te = time.perf_counter() - te
+        n_ex = len(ex_prompts)
+        mean = model.project_heads(zsum) / n_ex
+    else:
+        g = torch.Generator(device=dev).manual_seed(4321)
+        mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
 
     prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
     units_per_step = len(prompts) * cfg.n_layers * cfg.n_heads
@@ -125,6 +145,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    model.profile(True)  # HIP events around every GEMM launch of the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -142,18 +163,25 @@ def main():
     total_units = units_per_step * args.steps * world
     value = total_units / elapsed
 
-    # --- roofline: one more (untimed) step with HIP events around every GEMM
-    model.profile(True)
-    step()
-    torch.cuda.synchronize()
+    # --- roofline of the dominant kernel, from the timed region's events
     st = model.profile_stats()
     model.profile(False)
-    achieved = st["gemm_flops"] / (st["gemm_ms"] * 1e-3) / 1e12
+    fam = st["all"]
+    achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic()
     T = len(prompts[0])
     L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
     # F_alg(site at layer l) = (L-1-l)(2 P_l T + 2 T(T+1) d) + 2 d V
     f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
+    variants = {}
+    for name in ("qkv_mlpin", "o_mlpout", "unembed"):
+        v = st[name]
+        if v["launches"]:
+            variants[name] = {"launches": v["launches"],
+                              "achieved_tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2),
+                              "avg_launch_ms": round(v["ms"] / v["launches"], 4),
+                              "share_of_gemm_time": round(v["ms"] / fam["ms"], 4)}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -175,21 +203,24 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32)",
+            "kernel": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused epilogues)",
             "achieved": round(achieved, 2),
             "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None,
-            "launches_per_step": st["gemm_launches"],
-            "avg_launch_gflop": round(st["gemm_flops"] / max(st["gemm_launches"], 1) / 1e9, 3),
-            "avg_launch_ms": round(st["gemm_ms"] / max(st["gemm_launches"], 1), 4),
-            "gemm_share_of_step": round(st["gemm_ms"] / (elapsed / args.steps * 1e3), 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": round(fam["bytes"] / max(fam["launches"], 1)),
+            "launches_per_step": fam["launches"] // args.steps,
+            "avg_launch_gflop": round(fam["flops"] / max(fam["launches"], 1) / 1e9, 3),
+            "avg_launch_ms": round(fam["ms"] / max(fam["launches"], 1), 4),
+            "gemm_share_of_step": round(fam["ms"] / (elapsed / args.steps * 1e3), 4),
+            "variants": variants,
         },
         "algorithmic": {
             "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(value / world * f_alg / 1e12, 2),
-            "extraction_prompts_per_s": round(len(ex_prompts) / te, 1),
+            "extraction_prompts_per_s": round(n_ex / te, 1) if te else None,
         },
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -177,10 +177,12 @@ int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
  * and returns totals since the last enable; used by bench.py for the
  * roofline's achieved TFLOP/s of the dominant kernel. */
 typedef struct tvr_kernel_stats {
-  int64_t gemm_launches;
-  double gemm_flops;   /* algorithmic 2*M*N*K summed over launches */
-  double gemm_ms;      /* summed launch durations */
-  double gemm_bytes;   /* minimal operand bytes (A + W + C) summed */
+  /* index = GEMM epilogue: 0 unembed (bias), 1 QKV+MLP-in (split + GELU),
+   * 2 O+MLP-out (bias + parallel residual) */
+  int64_t gemm_launches[3];
+  double gemm_flops[3];   /* algorithmic 2*M*N*K summed over launches */
+  double gemm_ms[3];      /* summed launch durations */
+  double gemm_bytes[3];   /* minimal operand bytes (A + W + C) summed */
 } tvr_kernel_stats;
 int tvr_profile_enable(tvr_model* model, int32_t on);
 int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);

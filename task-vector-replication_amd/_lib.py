@@ -49,8 +49,11 @@ SITE_FIELDS = [f for f, _ in CSite._fields_]
 
 
 class CKernelStats(ctypes.Structure):
-    _fields_ = [("gemm_launches", ctypes.c_int64), ("gemm_flops", ctypes.c_double),
-                ("gemm_ms", ctypes.c_double), ("gemm_bytes", ctypes.c_double)]
+    _fields_ = [("gemm_launches", ctypes.c_int64 * 3), ("gemm_flops", ctypes.c_double * 3),
+                ("gemm_ms", ctypes.c_double * 3), ("gemm_bytes", ctypes.c_double * 3)]
+
+
+GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
 SIGNATURES = {

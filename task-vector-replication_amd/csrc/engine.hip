@@ -87,7 +87,7 @@ struct tvr_model {
   Staging staging;
   // profiling (tvr_profile_enable): event pairs around GEMM launches
   bool prof = false;
-  struct ProfRec { hipEvent_t a, b; double flops, bytes; };
+  struct ProfRec { hipEvent_t a, b; int epi; double flops, bytes; };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
 };
@@ -187,15 +187,15 @@ hipEvent_t prof_event(tvr_model* m) {
 int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M, int N,
                 int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr) {
   if (M <= 0 || N <= 0) return TVR_OK;
+  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (K=" +
+                                         std::to_string(K) + ")");
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (m && m->prof) {
     ev0 = prof_event(m);
     ev1 = prof_event(m);
     if (ev0) TVR_HIP(hipEventRecord(ev0, st));
   }
-  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0)
-    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (K=" +
-                                         std::to_string(K) + ")");
   const dim3 grid(gemm_grid(M, N)), block(GEMM_THREADS);
   switch (epi) {
     case EPI_BIAS:
@@ -211,7 +211,7 @@ int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
-    m->prof_recs.push_back({ev0, ev1, 2.0 * M * N * (double)K,
+    m->prof_recs.push_back({ev0, ev1, epi, 2.0 * M * N * (double)K,
                             4.0 * ((double)M * K + (double)N * K + (double)M * N)});
   }
   return TVR_OK;
@@ -413,10 +413,10 @@ int tvr_profile_read(tvr_model* m, tvr_kernel_stats* out) {
     TVR_HIP(hipEventSynchronize(r.b));
     float ms = 0.f;
     TVR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
-    s.gemm_launches += 1;
-    s.gemm_flops += r.flops;
-    s.gemm_bytes += r.bytes;
-    s.gemm_ms += ms;
+    s.gemm_launches[r.epi] += 1;
+    s.gemm_flops[r.epi] += r.flops;
+    s.gemm_bytes[r.epi] += r.bytes;
+    s.gemm_ms[r.epi] += ms;
   }
   *out = s;
   return TVR_OK;

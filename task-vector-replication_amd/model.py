@@ -243,8 +243,10 @@ class Model(TokenizerMixin):
     def profile_stats(self) -> dict:
         st = _lib.CKernelStats()
         _lib.check(self._lib.tvr_profile_read(self._h, ctypes.byref(st)), "tvr_profile_read")
-        return {"gemm_launches": st.gemm_launches, "gemm_flops": st.gemm_flops, "gemm_ms": st.gemm_ms,
-                "gemm_bytes": st.gemm_bytes}
+        per = {name: {"launches": st.gemm_launches[i], "flops": st.gemm_flops[i], "ms": st.gemm_ms[i],
+                      "bytes": st.gemm_bytes[i]} for i, name in enumerate(_lib.GEMM_VARIANTS)}
+        per["all"] = {k: sum(v[k] for v in per.values()) for k in ("launches", "flops", "ms", "bytes")}
+        return per
 
     # ------------------------------------------------- TL-style conveniences
     def _as_ids(self, tokens) -> List[int]:

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of a bench.py run into profiles/.
+
+  python tools/prof_summary.py --tag r01 --stats gpurun_out/prof_r1 \
+      --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write
+
+* kernel stats (--kernel-trace --stats): per kernel calls / total / avg ms
+* PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs, as the MI355X guide
+  prescribes): HBM bytes per GEMM launch = 2 x FETCH_SIZE x 1024 (gfx950
+  reports half the bytes of 16-B/lane streaming reads) + WRITE_SIZE x 1024,
+  next to the launch's algorithmic bytes (A + W + C, fp32).
+Writes profiles/rocprof_<tag>.json, profiles/kernel_stats_<tag>.csv and
+profiles/pmc_gemm_latest.json (read by bench.py for roofline.traffic).
+"""
+import argparse
+import csv
+import glob
+import json
+import shutil
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+# N-tiles (128 wide), K, N of each GEMM epilogue at Pythia-2.8B
+SHAPES = {"0": ("unembed", 2560, 50304), "1": ("qkv_mlpin", 2560, 17920), "2": ("o_mlpout", 12800, 2560)}
+
+
+def one(d, pattern):
+    hits = glob.glob(str(Path(d) / pattern))
+    if not hits:
+        raise SystemExit(f"no {pattern} under {d}")
+    return hits[0]
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def gemm_variant(name):
+    if "gemm_f32_nt_kernel<" not in name:
+        return None
+    return name.split("gemm_f32_nt_kernel<")[1][0]
+
+
+def pmc(d):
+    rows = []
+    for r in csv.DictReader(open(one(d, "*counter_collection.csv"))):
+        rows.append(r)
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--cmd", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline")
+    a = ap.parse_args()
+    out_dir = ROOT / "profiles"
+    out_dir.mkdir(exist_ok=True)
+    stats_csv = one(a.stats, "*kernel_stats.csv")
+    shutil.copy(stats_csv, out_dir / f"kernel_stats_{a.tag}.csv")
+    kernels = []
+    for r in csv.DictReader(open(stats_csv)):
+        kernels.append({"kernel": short(r["Name"]), "calls": int(r["Calls"]),
+                        "total_ms": round(int(r["TotalDurationNs"]) / 1e6, 3),
+                        "avg_ms": round(float(r["AverageNs"]) / 1e6, 4), "pct": round(float(r["Percentage"]), 2)})
+    summary = {"command": a.cmd, "kernels": kernels[:20]}
+    gemm = [k for k in kernels if "gemm_f32_nt_kernel" in k["kernel"]]
+    tot_calls = sum(k["calls"] for k in gemm)
+    summary["gemm_family"] = {"calls": tot_calls, "total_ms": round(sum(k["total_ms"] for k in gemm), 3),
+                              "avg_ms": round(sum(k["total_ms"] for k in gemm) / max(tot_calls, 1), 4)}
+    if a.fetch and a.write:
+        f, w = pmc(a.fetch), pmc(a.write)
+        per = {}
+        for rf, rw in zip(f, w):
+            v = gemm_variant(rf["Kernel_Name"])
+            if v is None:
+                continue
+            name, K, N = SHAPES[v]
+            tiles = int(rf["Grid_Size"]) // 256
+            M = (tiles // ((N + 127) // 128)) * 128
+            alg = 4.0 * (M * K + N * K + M * N)
+            hbm = 2.0 * float(rf["Counter_Value"]) * 1024 + float(rw["Counter_Value"]) * 1024
+            p = per.setdefault(name, {"launches": 0, "hbm_bytes": 0.0, "alg_bytes": 0.0})
+            p["launches"] += 1
+            p["hbm_bytes"] += hbm
+            p["alg_bytes"] += alg
+        n = sum(p["launches"] for p in per.values())
+        hbm = sum(p["hbm_bytes"] for p in per.values())
+        alg = sum(p["alg_bytes"] for p in per.values())
+        pm = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}",
+              "hbm_bytes_per_launch": round(hbm / n), "alg_bytes_per_launch": round(alg / n),
+              "ratio_hbm_to_alg": round(hbm / alg, 2), "launches": n,
+              "variants": {k: {"launches": p["launches"], "hbm_bytes_per_launch": round(p["hbm_bytes"] / p["launches"]),
+                               "alg_bytes_per_launch": round(p["alg_bytes"] / p["launches"]),
+                               "ratio": round(p["hbm_bytes"] / p["alg_bytes"], 2)} for k, p in per.items()}}
+        summary["pmc_gemm"] = pm
+        (out_dir / "pmc_gemm_latest.json").write_text(json.dumps(pm, indent=1) + "\n")
+    (out_dir / f"rocprof_{a.tag}.json").write_text(json.dumps(summary, indent=1) + "\n")
+    print(json.dumps(summary, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
