@@ -49,6 +49,9 @@ struct GemmEpi {
   int n_split;
   const float* resid;
   int ldr;
+  // Diagnostics only (tools/gemm_probe.hip; the engine passes nullptr): per
+  // block {Δs_memtime, Δs_memrealtime} to read the shader clock under load.
+  unsigned long long* stamps;
 };
 
 __device__ __forceinline__ float gelu_erf(float x) {
@@ -68,6 +71,8 @@ __global__ void __launch_bounds__(GEMM_THREADS, 2)
 gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
                    const float* __restrict__ W, int ldw, int M, int N, int K,
                    GemmEpi ep) {
+  const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   __shared__ __attribute__((aligned(16))) float sA[2][GEMM_BM * GEMM_LDK];
   __shared__ __attribute__((aligned(16))) float sB[2][GEMM_BN * GEMM_LDK];
 
@@ -190,6 +195,10 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
   store(acc01, 0, 1);
   store(acc10, 1, 0);
   store(acc11, 1, 1);
+  if (ep.stamps && t == 0) {
+    ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
+    ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+  }
 }
 
 inline int gemm_grid(int M, int N) {
