@@ -196,18 +196,22 @@ int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M
     ev1 = prof_event(m);
     if (ev0) TVR_HIP(hipEventRecord(ev0, st));
   }
-  const dim3 grid(gemm_grid(M, N)), block(GEMM_THREADS);
+  const bool large = gemm_use_large(M, N);
+#define TVR_GEMM_LAUNCH(E, TL)                                                                  \
+  hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
+                     st, A, lda, W, ldw, M, N, K, ep)
   switch (epi) {
     case EPI_BIAS:
-      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_BIAS>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      if (large) TVR_GEMM_LAUNCH(EPI_BIAS, TileLarge); else TVR_GEMM_LAUNCH(EPI_BIAS, TileSmall);
       break;
     case EPI_SPLIT_GELU:
-      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_SPLIT_GELU>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      if (large) TVR_GEMM_LAUNCH(EPI_SPLIT_GELU, TileLarge); else TVR_GEMM_LAUNCH(EPI_SPLIT_GELU, TileSmall);
       break;
     default:
-      hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_RESID>, grid, block, 0, st, A, lda, W, ldw, M, N, K, ep);
+      if (large) TVR_GEMM_LAUNCH(EPI_RESID, TileLarge); else TVR_GEMM_LAUNCH(EPI_RESID, TileSmall);
       break;
   }
+#undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));

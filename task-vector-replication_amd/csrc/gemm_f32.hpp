@@ -10,8 +10,13 @@
 // TransformerLens (scratch2.py:96,123,191 → TL attention/MLP).
 //
 // Design (gfx950):
-//   * 128x128 block tile, BK = 32, 256 threads = 4 waves in a 2x2 grid, each
-//     wave owns a 64x64 sub-tile = 2x2 accumulators of 32x32 (64 AGPRs).
+//   * Two block tiles (BK = 32, each wave owns TM x TN accumulators of 32x32):
+//       large 256x256, 512 threads = 8 waves (2 x 4), wave tile 128x64, 1 block/CU
+//       small 128x128, 256 threads = 4 waves (2 x 2), wave tile 64x64, 2 blocks/CU
+//     The large tile halves the bytes streamed per FLOP: with most panel reads
+//     missing L2 (blocks drift apart in k), the 128x128 tile's ~8 B/clk/CU of
+//     beyond-L2 demand capped it at ~78% of the (measured, DVFS-free) fp32
+//     MFMA peak; the small tile serves launches too small to fill 256 CUs.
 //   * f32-in MFMA is exact fp32 (bit-for-bit a k-ordered fmaf chain), 64
 //     FLOP/clk/SIMD, so this is the only matrix path that keeps the
 //     reference's fp32 numerics.
@@ -59,25 +64,37 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-constexpr int GEMM_BM = 128;
-constexpr int GEMM_BN = 128;
 constexpr int GEMM_BK = 32;
 constexpr int GEMM_LDK = GEMM_BK + 4;  // padded LDS row (floats)
 constexpr int GEMM_GROUP_M = 8;
-constexpr int GEMM_THREADS = 256;
 
-template <int EPI>
-__global__ void __launch_bounds__(GEMM_THREADS, 2)
+template <int BM_, int BN_, int WM_, int WN_>
+struct GemmTile {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int THREADS = WM * WN * 64;
+  static constexpr int TM = BM / WM / 32;  // 32x32 accumulators per wave (M)
+  static constexpr int TN = BN / WN / 32;  // (N)
+  static constexpr int LOADS_A = BM * GEMM_BK / 4 / THREADS;  // float4 per thread per K step
+  static constexpr int LOADS_B = BN * GEMM_BK / 4 / THREADS;
+  static_assert(LOADS_A * THREADS * 4 == BM * GEMM_BK && LOADS_B * THREADS * 4 == BN * GEMM_BK, "staging map");
+};
+using TileLarge = GemmTile<256, 256, 2, 4>;
+using TileSmall = GemmTile<128, 128, 2, 2>;
+
+// 2 waves per SIMD for both tiles (8 waves per CU).
+template <int EPI, class TL>
+__global__ void __launch_bounds__(TL::THREADS, 2)
 gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
                    const float* __restrict__ W, int ldw, int M, int N, int K,
                    GemmEpi ep) {
+  constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN, NT = TL::THREADS;
   const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;
   const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  __shared__ __attribute__((aligned(16))) float sA[2][GEMM_BM * GEMM_LDK];
-  __shared__ __attribute__((aligned(16))) float sB[2][GEMM_BN * GEMM_LDK];
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * GEMM_LDK];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN * GEMM_LDK];
 
-  const int nbm = (M + GEMM_BM - 1) / GEMM_BM;
-  const int nbn = (N + GEMM_BN - 1) / GEMM_BN;
+  const int nbm = (M + BM - 1) / BM;
+  const int nbn = (N + BN - 1) / BN;
   const int nwg = nbm * nbn;
   const int bid = blockIdx.x;
   // Blocks b and b+8 share an XCD (round-robin dispatch): give each of the 8
@@ -91,43 +108,47 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
   const int in_grp = wg - grp * per_group;
   const int tm = first_m + in_grp % gsz;
   const int tn = in_grp / gsz;
-  const int m0 = tm * GEMM_BM, n0 = tn * GEMM_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const int t = threadIdx.x;
-  // staging map: 4 float4 of A and 4 of W per thread per K step
-  const float* ga[4];
-  const float* gw[4];
-  int soff[4];
+  // staging map: row = f / 8, 4 floats at column (f % 8) * 4 of the BK slice
+  const float* ga[TL::LOADS_A];
+  const float* gw[TL::LOADS_B];
+  int sa[TL::LOADS_A], sb[TL::LOADS_B];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int f = t + GEMM_THREADS * i;
-    const int row = f >> 3, c = (f & 7) * 4;
-    const int am = min(m0 + row, M - 1);
-    const int wn = min(n0 + row, N - 1);
-    ga[i] = A + (size_t)am * lda + c;
-    gw[i] = W + (size_t)wn * ldw + c;
-    soff[i] = row * GEMM_LDK + c;
+  for (int i = 0; i < TL::LOADS_A; ++i) {
+    const int f = t + NT * i, row = f >> 3, c = (f & 7) * 4;
+    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + c;
+    sa[i] = row * GEMM_LDK + c;
+  }
+#pragma unroll
+  for (int i = 0; i < TL::LOADS_B; ++i) {
+    const int f = t + NT * i, row = f >> 3, c = (f & 7) * 4;
+    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + c;
+    sb[i] = row * GEMM_LDK + c;
   }
 
   const int wave = t >> 6, lane = t & 63;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / TL::WN, wc = wave % TL::WN;
   const int lr = lane & 31, lh = lane >> 5;
-  const int aoff = (wr * 64 + lr) * GEMM_LDK + lh * 4;
-  const int boff = (wc * 64 + lr) * GEMM_LDK + lh * 4;
+  const int aoff = (wr * (BM / TL::WM) + lr) * GEMM_LDK + lh * 4;
+  const int boff = (wc * (BN / TL::WN) + lr) * GEMM_LDK + lh * 4;
 
-  f32x16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
-  f32x4 ra[4], rb[4];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  f32x4 ra[TL::LOADS_A], rb[TL::LOADS_B];
 
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    ra[i] = *(const f32x4*)(ga[i]);
-    rb[i] = *(const f32x4*)(gw[i]);
-  }
+  for (int i = 0; i < TL::LOADS_A; ++i) ra[i] = *(const f32x4*)(ga[i]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    *(f32x4*)(&sA[0][soff[i]]) = ra[i];
-    *(f32x4*)(&sB[0][soff[i]]) = rb[i];
-  }
+  for (int i = 0; i < TL::LOADS_B; ++i) rb[i] = *(const f32x4*)(gw[i]);
+#pragma unroll
+  for (int i = 0; i < TL::LOADS_A; ++i) *(f32x4*)(&sA[0][sa[i]]) = ra[i];
+#pragma unroll
+  for (int i = 0; i < TL::LOADS_B; ++i) *(f32x4*)(&sB[0][sb[i]]) = rb[i];
   __syncthreads();
 
   const int nk = K / GEMM_BK;
@@ -137,72 +158,75 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
     if (more) {
       const int k1 = (kt + 1) * GEMM_BK;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ra[i] = *(const f32x4*)(ga[i] + k1);
-        rb[i] = *(const f32x4*)(gw[i] + k1);
-      }
+      for (int i = 0; i < TL::LOADS_A; ++i) ra[i] = *(const f32x4*)(ga[i] + k1);
+#pragma unroll
+      for (int i = 0; i < TL::LOADS_B; ++i) rb[i] = *(const f32x4*)(gw[i] + k1);
     }
     const float* pa = &sA[buf][aoff];
     const float* pb = &sB[buf][boff];
 #pragma unroll
     for (int kk = 0; kk < GEMM_BK / 8; ++kk) {
-      const f32x4 a0 = *(const f32x4*)(pa + kk * 8);
-      const f32x4 a1 = *(const f32x4*)(pa + 32 * GEMM_LDK + kk * 8);
-      const f32x4 b0 = *(const f32x4*)(pb + kk * 8);
-      const f32x4 b1 = *(const f32x4*)(pb + 32 * GEMM_LDK + kk * 8);
+      f32x4 a[TM], b[TN];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc00, 0, 0, 0);
-        acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc01, 0, 0, 0);
-        acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc10, 0, 0, 0);
-        acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc11, 0, 0, 0);
-      }
+      for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(pa + i * 32 * GEMM_LDK + kk * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(pb + j * 32 * GEMM_LDK + kk * 8);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
     }
     if (more) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        *(f32x4*)(&sA[buf ^ 1][soff[i]]) = ra[i];
-        *(f32x4*)(&sB[buf ^ 1][soff[i]]) = rb[i];
-      }
+      for (int i = 0; i < TL::LOADS_A; ++i) *(f32x4*)(&sA[buf ^ 1][sa[i]]) = ra[i];
+#pragma unroll
+      for (int i = 0; i < TL::LOADS_B; ++i) *(f32x4*)(&sB[buf ^ 1][sb[i]]) = rb[i];
     }
     __syncthreads();
     buf ^= 1;
   }
 
   // Epilogue.  32x32 C/D map: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-  auto store = [&](const f32x16& acc, int mi, int ni) {
-    const int col = n0 + wc * 64 + ni * 32 + lr;
-    if (col >= N) return;
-    const float b = ep.bias ? ep.bias[col] : 0.0f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (row >= M) continue;
-      const float v = acc[r] + b;
-      if constexpr (EPI == EPI_BIAS) {
-        ep.out0[(size_t)row * ep.ld0 + col] = v;
-      } else if constexpr (EPI == EPI_SPLIT_GELU) {
-        if (col < ep.n_split)
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wc * (BN / TL::WN) + j * 32 + lr;
+    if (col >= N) continue;
+    const float bcol = ep.bias ? ep.bias[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wr * (BM / TL::WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= M) continue;
+        const float v = acc[i][j][r] + bcol;
+        if constexpr (EPI == EPI_BIAS) {
           ep.out0[(size_t)row * ep.ld0 + col] = v;
-        else
-          ep.out1[(size_t)row * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
-      } else {
-        ep.out0[(size_t)row * ep.ld0 + col] = v + ep.resid[(size_t)row * ep.ldr + col];
+        } else if constexpr (EPI == EPI_SPLIT_GELU) {
+          if (col < ep.n_split)
+            ep.out0[(size_t)row * ep.ld0 + col] = v;
+          else
+            ep.out1[(size_t)row * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
+        } else {
+          ep.out0[(size_t)row * ep.ld0 + col] = v + ep.resid[(size_t)row * ep.ldr + col];
+        }
       }
     }
-  };
-  store(acc00, 0, 0);
-  store(acc01, 0, 1);
-  store(acc10, 1, 0);
-  store(acc11, 1, 1);
+  }
   if (ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
   }
 }
 
+template <class TL>
 inline int gemm_grid(int M, int N) {
-  return ((M + GEMM_BM - 1) / GEMM_BM) * ((N + GEMM_BN - 1) / GEMM_BN);
+  return ((M + TL::BM - 1) / TL::BM) * ((N + TL::BN - 1) / TL::BN);
 }
+
+// The large tile once it fills every CU at least twice, else the small one.
+inline bool gemm_use_large(int M, int N) { return gemm_grid<TileLarge>(M, N) >= 512; }
 
 }  // namespace tvr

@@ -28,7 +28,8 @@ def rel_err(a, b):
 
 # ------------------------------------------------------------------ kernels
 @pytest.mark.parametrize("M,N,K", [(1, 1, 32), (37, 130, 64), (128, 128, 32), (300, 257, 320),
-                                   (1000, 2560, 2560), (129, 50304, 64)])
+                                   (1000, 2560, 2560), (129, 50304, 64),
+                                   (4096, 8192, 256), (3001, 17920, 96), (1025, 50304, 64)])
 def test_gemm_f32_matches_torch(M, N, K):
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
     A = torch.randn(M, K, generator=g)

@@ -29,7 +29,8 @@ int main(int argc, char** argv) {
   for (auto& s : shapes) {
     float *A, *W, *C, *C2, *b;
     unsigned long long* stamps;
-    const int nblk = gemm_grid(s.M, s.N);
+    const bool large = gemm_use_large(s.M, s.N);
+    const int nblk = large ? gemm_grid<TileLarge>(s.M, s.N) : gemm_grid<TileSmall>(s.M, s.N);
     hipMalloc(&A, sizeof(float) * (size_t)s.M * s.K);
     hipMalloc(&W, sizeof(float) * (size_t)s.N * s.K);
     hipMalloc(&C, sizeof(float) * (size_t)s.M * s.N);
@@ -45,10 +46,13 @@ int main(int argc, char** argv) {
     ep.n_split = 7680; ep.resid = C; ep.ldr = s.N;
     auto launch = [&](unsigned long long* st) {
       ep.stamps = st;
-      if (s.epi == EPI_SPLIT_GELU)
-        hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_SPLIT_GELU>, dim3(nblk), dim3(GEMM_THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
-      else
-        hipLaunchKernelGGL(gemm_f32_nt_kernel<EPI_RESID>, dim3(nblk), dim3(GEMM_THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
+      if (s.epi == EPI_SPLIT_GELU) {
+        if (large) hipLaunchKernelGGL((gemm_f32_nt_kernel<EPI_SPLIT_GELU, TileLarge>), dim3(nblk), dim3(TileLarge::THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
+        else hipLaunchKernelGGL((gemm_f32_nt_kernel<EPI_SPLIT_GELU, TileSmall>), dim3(nblk), dim3(TileSmall::THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
+      } else {
+        if (large) hipLaunchKernelGGL((gemm_f32_nt_kernel<EPI_RESID, TileLarge>), dim3(nblk), dim3(TileLarge::THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
+        else hipLaunchKernelGGL((gemm_f32_nt_kernel<EPI_RESID, TileSmall>), dim3(nblk), dim3(TileSmall::THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, ep);
+      }
     };
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
@@ -68,8 +72,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < nblk; ++i) if (h[2 * i + 1]) mhz.push_back(h[2 * i] / (double)h[2 * i + 1] * 100.0);
     std::sort(mhz.begin(), mhz.end());
     const double tf = 2.0 * s.M * (double)s.N * s.K * reps / (ms * 1e-3) / 1e12;
-    printf("{\"shape\": \"%s\", \"tflops\": %.2f, \"ms_per_launch\": %.3f, \"clock_mhz_median\": %.0f, "
-           "\"peak_at_clock\": %.1f, \"frac_of_clock_peak\": %.3f}\n", s.name, tf, ms / reps, mhz[mhz.size() / 2],
+    printf("{\"tile\": \"%s\", \"shape\": \"%s\", \"tflops\": %.2f, \"ms_per_launch\": %.3f, \"clock_mhz_median\": %.0f, "
+           "\"peak_at_clock\": %.1f, \"frac_of_clock_peak\": %.3f}\n", large ? "256x256" : "128x128", s.name, tf, ms / reps, mhz[mhz.size() / 2],
            1024 * 64.0 * mhz[mhz.size() / 2] * 1e6 / 1e12, tf / (1024 * 64.0 * mhz[mhz.size() / 2] * 1e6 / 1e12));
     hipFree(A); hipFree(W); hipFree(C); hipFree(C2); hipFree(b); hipFree(stamps);
   }
