@@ -241,12 +241,27 @@ struct Acts {
   float* a2;      // [R][K2]  (z | gelu(mlp-in))
 };
 
+int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
+                     int n_seqs, int maxT, float* z, hipStream_t st) {
+  if (n_seqs <= 0) return TVR_OK;
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model;
+  const size_t smem = attention_smem_bytes(maxT, c.d_head);
+  if (smem > 64 * 1024)
+    TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)smem));
+  hipLaunchKernelGGL(attention_kernel, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
+                     cache_qkv, 3 * d, d_seqs, z, m->K2, m->rot_cos, m->rot_sin, d, c.d_head, c.rotary_dim,
+                     1.0f / std::sqrt((float)c.d_head));
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
 // One transformer block over the first R rows (Pythia parallel residual):
 //   x = LNPre(resid); [qkv | h] = x @ W1^T + b1; z = attn(qkv); resid += [z|gelu h] @ W2^T + b2
+// (run_block computes up to z; run_block_out the second projection.)
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
-              Acts& a, float* qkv_out, const float* cache_qkv, hipStream_t st,
-              const float* z_dst_capture_unused = nullptr) {
-  (void)z_dst_capture_unused;
+              Acts& a, float* qkv_out, const float* cache_qkv, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -259,18 +274,49 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   e1.ld1 = m->K2;
   e1.n_split = 3 * d;
   TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1, d, R, m->D1, d, e1, st, m));
-  if (n_seqs > 0) {
-    const size_t smem = attention_smem_bytes(maxT, c.d_head);
-    if (smem > 64 * 1024)
-      TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    hipLaunchKernelGGL(attention_kernel, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st,
-                       qkv_out, 3 * d, cache_qkv, 3 * d, d_seqs, a.a2, m->K2, m->rot_cos,
-                       m->rot_sin, d, c.d_head, c.rotary_dim,
-                       1.0f / std::sqrt((float)c.d_head));
-    TVR_HIP(hipGetLastError());
-  }
-  return TVR_OK;
+  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st);
+}
+
+// The last layer when only each sequence's LAST row is read afterwards (patch
+// sweeps, extraction): every row still needs K and V (they are attended to),
+// but Q, the MLP, attention output and the second projection are computed for
+// the n_last rows listed in d_last only (~5% of a CIE sweep's FLOPs saved).
+// d_seqs must carry q0 = n - 1.  write_out = false skips the second projection
+// (nothing downstream reads the final residual).
+int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT, Acts& a,
+                        const float* cache_qkv, const int32_t* d_last, int n_last, bool write_out,
+                        hipStream_t st) {
+  const tvr_config& c = m->cfg;
+  const int d = c.d_model;
+  const tvr_layer_weights& w = m->layers[l];
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, st));
+  GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row
+  kv.bias = w.b1 + d;
+  kv.out0 = a.qkv + d;
+  kv.ld0 = 3 * d;
+  kv.n_split = 2 * d;
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1 + (size_t)d * d, d, R, 2 * d, d, kv, st, m));
+  GemmEpi e1{};  // all columns for the last rows, gathered and scattered in place
+  e1.bias = w.b1;
+  e1.out0 = a.qkv;
+  e1.ld0 = 3 * d;
+  e1.out1 = a.a2 + d;
+  e1.ld1 = m->K2;
+  e1.n_split = 3 * d;
+  e1.a_rows = d_last;
+  e1.out_rows = d_last;
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1, d, n_last, m->D1, d, e1, st, m));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st));
+  if (!write_out) return TVR_OK;
+  GemmEpi e2{};
+  e2.bias = w.b2;
+  e2.out0 = a.resid;
+  e2.ld0 = d;
+  e2.resid = a.resid;
+  e2.ldr = d;
+  e2.a_rows = d_last;
+  e2.out_rows = d_last;
+  return launch_gemm(EPI_RESID, a.a2, m->K2, w.w2, m->K2, n_last, d, m->K2, e2, st, m);
 }
 
 int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
@@ -504,7 +550,11 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
     return fail(TVR_ERR_UNSUPPORTED, "attention LDS budget exceeded");
 
   std::vector<SeqDesc> seqs(n_seq);
-  for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1};
+  for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1, 0, 0};
+  // without a trace only each prompt's last row is read after the last layer
+  const bool trim = trace == nullptr;
+  std::vector<SeqDesc> seqs_last(seqs);
+  for (auto& q : seqs_last) q.q0 = q.n - 1;
   std::vector<int32_t> tg(n_seq, -1);
   if (targets) std::copy(targets, targets + n_seq, tg.begin());
   std::vector<int32_t> tok(tokens, tokens + R);
@@ -512,6 +562,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   const int FC = std::min(kFinalChunk, n_seq);
   Carve cv;
   const size_t o_seqs = cv.take<SeqDesc>(n_seq);
+  const size_t o_seqs_last = cv.take<SeqDesc>(n_seq);
   const size_t o_tok = cv.take<int32_t>(R);
   const size_t o_last = cv.take<int32_t>(n_seq);
   const size_t o_tg = cv.take<int32_t>(n_seq);
@@ -526,6 +577,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   char* base = m->ws;
   UploadBatch ub;
   ub.add(o_seqs, seqs);
+  ub.add(o_seqs_last, seqs_last);
   ub.add(o_tok, tok);
   ub.add(o_last, last);
   ub.add(o_tg, tg);
@@ -549,7 +601,13 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
       TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, (size_t)R * d * sizeof(float),
                              hipMemcpyDeviceToDevice, st));
     float* qkv = trace ? trace->qkv + (size_t)l * 3 * tstride : a.qkv;
-    TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, st));
+    const bool want_out = out_prob || out_topk || out_logits;
+    if (trim && l == L - 1) {
+      TVR_TRY(run_block_last_rows(m, l, R, (const SeqDesc*)(base + o_seqs_last), n_seq, maxT, a, nullptr,
+                                  d_last, n_seq, want_out, st));
+    } else {
+      TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, st));
+    }
     if (capture_zsum) {
       float* part = (float*)(base + o_cap);
       hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
@@ -561,7 +619,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
     if (trace)
       TVR_HIP(hipMemcpy2DAsync(trace->z + l * tstride, d * sizeof(float), a.a2, m->K2 * sizeof(float),
                                d * sizeof(float), R, hipMemcpyDeviceToDevice, st));
-    TVR_TRY(run_block_out(m, l, R, a, st));
+    if (!(trim && l == L - 1)) TVR_TRY(run_block_out(m, l, R, a, st));
   }
   if (trace) {
     TVR_HIP(hipMemcpyAsync(trace->resid + L * tstride, a.resid, (size_t)R * d * sizeof(float),
@@ -652,7 +710,7 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     const int i = order[k];
     const tvr_site& s = sites[i];
     const int srow = trace->seq_off[s.seq];
-    seqs[k] = {row0[i], nrow[i], p0[i], srow};
+    seqs[k] = {row0[i], nrow[i], p0[i], srow, 0, 0};
     EntryDesc e{};
     e.kind = s.kind;
     e.row0 = row0[i];
@@ -665,15 +723,22 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     e.vec = s.vec;
     ents[k] = e;
   }
-  std::vector<int32_t> last(n_sites), tg(n_sites);
+  std::vector<int32_t> last(n_sites), tg(n_sites), last_sorted(n_sites);
   for (int i = 0; i < n_sites; ++i) {
     last[i] = row0[i] + nrow[i] - 1;
     tg[i] = sites[i].target;
+  }
+  std::vector<SeqDesc> seqs_last(seqs);
+  for (int k = 0; k < n_sites; ++k) {
+    seqs_last[k].q0 = seqs_last[k].n - 1;
+    last_sorted[k] = last[order[k]];
   }
 
   const int FC = std::min(kFinalChunk, n_sites);
   Carve cv;
   const size_t o_seqs = cv.take<SeqDesc>(n_sites);
+  const size_t o_seqs_last = cv.take<SeqDesc>(n_sites);
+  const size_t o_last_sorted = cv.take<int32_t>(n_sites);
   const size_t o_ents = cv.take<EntryDesc>(n_sites);
   const size_t o_last = cv.take<int32_t>(n_sites);
   const size_t o_tg = cv.take<int32_t>(n_sites);
@@ -689,6 +754,8 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   char* base = m->ws;
   UploadBatch ub;
   ub.add(o_seqs, seqs);
+  ub.add(o_seqs_last, seqs_last);
+  ub.add(o_last_sorted, last_sorted);
   ub.add(o_ents, ents);
   ub.add(o_last, last);
   ub.add(o_tg, tg);
@@ -717,9 +784,14 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     TVR_TRY(enter(l));
     const int Rl = rows_le[l];
     if (Rl == 0) continue;
-    TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv,
-                      trace->qkv + (size_t)l * 3 * tstride, st));
-    TVR_TRY(run_block_out(m, l, Rl, a, st));
+    const float* cache = trace->qkv + (size_t)l * 3 * tstride;
+    if (l == L - 1) {
+      TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), cnt_le[l], maxT, a, cache,
+                                  (const int32_t*)(base + o_last_sorted), cnt_le[l], true, st));
+    } else {
+      TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv, cache, st));
+      TVR_TRY(run_block_out(m, l, Rl, a, st));
+    }
   }
   TVR_TRY(enter(L));
   return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,

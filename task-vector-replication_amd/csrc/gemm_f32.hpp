@@ -33,6 +33,7 @@
 //     out-of-range rows/cols load clamped addresses and are never stored.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 namespace tvr {
 
@@ -54,6 +55,10 @@ struct GemmEpi {
   int n_split;
   const float* resid;
   int ldr;
+  // Optional row indirection (the trimmed last layer): A row m is read from
+  // a_rows[m], output row m (and its residual) lives at out_rows[m].
+  const int32_t* a_rows;
+  const int32_t* out_rows;
   // Diagnostics only (tools/gemm_probe.hip; the engine passes nullptr): per
   // block {Δs_memtime, Δs_memrealtime} to read the shader clock under load.
   unsigned long long* stamps;
@@ -118,7 +123,8 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
 #pragma unroll
   for (int i = 0; i < TL::LOADS_A; ++i) {
     const int f = t + NT * i, row = f >> 3, c = (f & 7) * 4;
-    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + c;
+    const int am = min(m0 + row, M - 1);
+    ga[i] = A + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + c;
     sa[i] = row * GEMM_LDK + c;
   }
 #pragma unroll
@@ -201,16 +207,17 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wr * (BM / TL::WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= M) continue;
+        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
         const float v = acc[i][j][r] + bcol;
         if constexpr (EPI == EPI_BIAS) {
-          ep.out0[(size_t)row * ep.ld0 + col] = v;
+          ep.out0[orow * ep.ld0 + col] = v;
         } else if constexpr (EPI == EPI_SPLIT_GELU) {
           if (col < ep.n_split)
-            ep.out0[(size_t)row * ep.ld0 + col] = v;
+            ep.out0[orow * ep.ld0 + col] = v;
           else
-            ep.out1[(size_t)row * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
+            ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
         } else {
-          ep.out0[(size_t)row * ep.ld0 + col] = v + ep.resid[(size_t)row * ep.ldr + col];
+          ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
         }
       }
     }

@@ -22,6 +22,8 @@ struct SeqDesc {
   int32_t n;          // number of computed rows
   int32_t p0;         // absolute position of row0
   int32_t cache_row;  // trace row of position 0 (for the K/V prefix), -1: none
+  int32_t q0;         // first computed row that is a query (n-1: last row only)
+  int32_t pad;
 };
 
 // How a patch site's residual is materialised at its entry layer e
@@ -158,7 +160,7 @@ attention_kernel(const float* __restrict__ qkv, int ldq,
   for (int j = wave; j < T; j += 4) rotate_row(Ks + j * dhp, j, rd, cos_t, sin_t, lane, 64);
   __syncthreads();
 
-  for (int ib = 0; ib < sd.n; ib += 4) {
+  for (int ib = sd.q0; ib < sd.n; ib += 4) {
     const int i = ib + wave;
     const bool act = i < sd.n;
     const int pos = sd.p0 + i;
