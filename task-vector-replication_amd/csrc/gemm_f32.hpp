@@ -69,34 +69,38 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-constexpr int GEMM_BK = 32;
-constexpr int GEMM_LDK = GEMM_BK + 4;  // padded LDS row (floats)
+constexpr int GEMM_BK = 32;  // K granule the host must respect (every tile's BK divides it)
 constexpr int GEMM_GROUP_M = 8;
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int BK_>
 struct GemmTile {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
+  static constexpr int LDK = BK + 4;  // padded LDS row (floats): conflict-free ds_read_b128
   static constexpr int THREADS = WM * WN * 64;
   static constexpr int TM = BM / WM / 32;  // 32x32 accumulators per wave (M)
   static constexpr int TN = BN / WN / 32;  // (N)
-  static constexpr int LOADS_A = BM * GEMM_BK / 4 / THREADS;  // float4 per thread per K step
-  static constexpr int LOADS_B = BN * GEMM_BK / 4 / THREADS;
-  static_assert(LOADS_A * THREADS * 4 == BM * GEMM_BK && LOADS_B * THREADS * 4 == BN * GEMM_BK, "staging map");
+  static constexpr int KK = BK / 8;        // k-groups of 8 per K step (one ds_read_b128 = 4 MFMAs)
+  static constexpr int C4 = BK / 4;        // float4 per staged row
+  static constexpr int LOADS_A = BM * BK / 4 / THREADS;  // float4 per thread per K step
+  static constexpr int LOADS_B = BN * BK / 4 / THREADS;
+  static_assert(LOADS_A * THREADS * 4 == BM * BK && LOADS_B * THREADS * 4 == BN * BK, "staging map");
+  static_assert(GEMM_BK % BK == 0, "BK must divide the host K granule");
 };
-using TileLarge = GemmTile<256, 256, 2, 4>;
-using TileSmall = GemmTile<128, 128, 2, 2>;
+using TileLarge = GemmTile<256, 256, 2, 4, 32>;
+using TileSmall = GemmTile<128, 128, 2, 2, 32>;
 
-// 2 waves per SIMD for both tiles (8 waves per CU).
+// 2 waves per SIMD for every tile (8 waves per CU).
 template <int EPI, class TL>
 __global__ void __launch_bounds__(TL::THREADS, 2)
 gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
                    const float* __restrict__ W, int ldw, int M, int N, int K,
                    GemmEpi ep) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN, NT = TL::THREADS;
+  constexpr int BK = TL::BK, LDK = TL::LDK, KK = TL::KK;
   const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;
   const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  __shared__ __attribute__((aligned(16))) float sA[2][BM * GEMM_LDK];
-  __shared__ __attribute__((aligned(16))) float sB[2][BN * GEMM_LDK];
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) float sB[2][BN * LDK];
 
   const int nbm = (M + BM - 1) / BM;
   const int nbn = (N + BN - 1) / BN;
@@ -116,29 +120,29 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int t = threadIdx.x;
-  // staging map: row = f / 8, 4 floats at column (f % 8) * 4 of the BK slice
+  // staging map: row = f / C4, 4 floats at column (f % C4) * 4 of the BK slice
   const float* ga[TL::LOADS_A];
   const float* gw[TL::LOADS_B];
   int sa[TL::LOADS_A], sb[TL::LOADS_B];
 #pragma unroll
   for (int i = 0; i < TL::LOADS_A; ++i) {
-    const int f = t + NT * i, row = f >> 3, c = (f & 7) * 4;
+    const int f = t + NT * i, row = f / TL::C4, c = (f % TL::C4) * 4;
     const int am = min(m0 + row, M - 1);
     ga[i] = A + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + c;
-    sa[i] = row * GEMM_LDK + c;
+    sa[i] = row * LDK + c;
   }
 #pragma unroll
   for (int i = 0; i < TL::LOADS_B; ++i) {
-    const int f = t + NT * i, row = f >> 3, c = (f & 7) * 4;
+    const int f = t + NT * i, row = f / TL::C4, c = (f % TL::C4) * 4;
     gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + c;
-    sb[i] = row * GEMM_LDK + c;
+    sb[i] = row * LDK + c;
   }
 
   const int wave = t >> 6, lane = t & 63;
   const int wr = wave / TL::WN, wc = wave % TL::WN;
   const int lr = lane & 31, lh = lane >> 5;
-  const int aoff = (wr * (BM / TL::WM) + lr) * GEMM_LDK + lh * 4;
-  const int boff = (wc * (BN / TL::WN) + lr) * GEMM_LDK + lh * 4;
+  const int aoff = (wr * (BM / TL::WM) + lr) * LDK + lh * 4;
+  const int boff = (wc * (BN / TL::WN) + lr) * LDK + lh * 4;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -146,52 +150,68 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
   f32x4 ra[TL::LOADS_A], rb[TL::LOADS_B];
+  f32x4 fa[TM], fb[TN];  // fragments of the k-group being multiplied
+
+  auto frags = [&](int b, int kk, f32x4 (&xa)[TM], f32x4 (&xb)[TN]) {
+    const float* pa = &sA[b][aoff + kk * 8];
+    const float* pb = &sB[b][boff + kk * 8];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) xa[i] = *(const f32x4*)(pa + i * 32 * LDK);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) xb[j] = *(const f32x4*)(pb + j * 32 * LDK);
+  };
+  auto stage = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < TL::LOADS_A; ++i) *(f32x4*)(&sA[b][sa[i]]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < TL::LOADS_B; ++i) *(f32x4*)(&sB[b][sb[i]]) = rb[i];
+  };
 
 #pragma unroll
   for (int i = 0; i < TL::LOADS_A; ++i) ra[i] = *(const f32x4*)(ga[i]);
 #pragma unroll
   for (int i = 0; i < TL::LOADS_B; ++i) rb[i] = *(const f32x4*)(gw[i]);
-#pragma unroll
-  for (int i = 0; i < TL::LOADS_A; ++i) *(f32x4*)(&sA[0][sa[i]]) = ra[i];
-#pragma unroll
-  for (int i = 0; i < TL::LOADS_B; ++i) *(f32x4*)(&sB[0][sb[i]]) = rb[i];
+  stage(0);
   __syncthreads();
+  frags(0, 0, fa, fb);
 
-  const int nk = K / GEMM_BK;
+  // Software-pipelined K loop: the fragments of k-group kk+1 are read before
+  // kk's MFMAs; at the last k-group the next tile is staged, the block
+  // synchronises and the NEXT step's first fragments are read, all ahead of
+  // the last group's MFMAs, whose 4*TM*TN MFMAs then cover the LDS latency.
+  const int nk = K / BK;
   int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = (kt + 1) < nk;
     if (more) {
-      const int k1 = (kt + 1) * GEMM_BK;
+      const int k1 = (kt + 1) * BK;
 #pragma unroll
       for (int i = 0; i < TL::LOADS_A; ++i) ra[i] = *(const f32x4*)(ga[i] + k1);
 #pragma unroll
       for (int i = 0; i < TL::LOADS_B; ++i) rb[i] = *(const f32x4*)(gw[i] + k1);
     }
-    const float* pa = &sA[buf][aoff];
-    const float* pb = &sB[buf][boff];
 #pragma unroll
-    for (int kk = 0; kk < GEMM_BK / 8; ++kk) {
-      f32x4 a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *(const f32x4*)(pa + i * 32 * GEMM_LDK + kk * 8);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *(const f32x4*)(pb + j * 32 * GEMM_LDK + kk * 8);
+    for (int kk = 0; kk < KK; ++kk) {
+      f32x4 na[TM], nb[TN];
+      if (kk + 1 < KK) {
+        frags(buf, kk + 1, na, nb);
+      } else if (more) {
+        stage(buf ^ 1);
+        __syncthreads();
+        frags(buf ^ 1, 0, na, nb);
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < TL::LOADS_A; ++i) *(f32x4*)(&sA[buf ^ 1][sa[i]]) = ra[i];
+      for (int i = 0; i < TM; ++i) fa[i] = na[i];
 #pragma unroll
-      for (int i = 0; i < TL::LOADS_B; ++i) *(f32x4*)(&sB[buf ^ 1][sb[i]]) = rb[i];
+      for (int j = 0; j < TN; ++j) fb[j] = nb[j];
     }
-    __syncthreads();
     buf ^= 1;
   }
 
