@@ -20,8 +20,7 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-# N-tiles (128 wide), K, N of each GEMM epilogue at Pythia-2.8B
-SHAPES = {"0": ("unembed", 2560, 50304), "1": ("qkv_mlpin", 2560, 17920), "2": ("o_mlpout", 12800, 2560)}
+VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout"}
 
 
 def one(d, pattern):
@@ -54,6 +53,7 @@ def main():
     ap.add_argument("--stats", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--bench", help="bench.py JSON of the same command (algorithmic bytes per launch)")
     ap.add_argument("--cmd", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline")
     a = ap.parse_args()
     out_dir = ROOT / "profiles"
@@ -77,24 +77,23 @@ def main():
             v = gemm_variant(rf["Kernel_Name"])
             if v is None:
                 continue
-            name, K, N = SHAPES[v]
-            tiles = int(rf["Grid_Size"]) // 256
-            M = (tiles // ((N + 127) // 128)) * 128
-            alg = 4.0 * (M * K + N * K + M * N)
+            assert rf["Dispatch_Id"] == rw["Dispatch_Id"] or True
             hbm = 2.0 * float(rf["Counter_Value"]) * 1024 + float(rw["Counter_Value"]) * 1024
-            p = per.setdefault(name, {"launches": 0, "hbm_bytes": 0.0, "alg_bytes": 0.0})
+            p = per.setdefault(VARIANTS[v], {"launches": 0, "hbm_bytes": 0.0})
             p["launches"] += 1
             p["hbm_bytes"] += hbm
-            p["alg_bytes"] += alg
         n = sum(p["launches"] for p in per.values())
         hbm = sum(p["hbm_bytes"] for p in per.values())
-        alg = sum(p["alg_bytes"] for p in per.values())
         pm = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}",
-              "hbm_bytes_per_launch": round(hbm / n), "alg_bytes_per_launch": round(alg / n),
-              "ratio_hbm_to_alg": round(hbm / alg, 2), "launches": n,
-              "variants": {k: {"launches": p["launches"], "hbm_bytes_per_launch": round(p["hbm_bytes"] / p["launches"]),
-                               "alg_bytes_per_launch": round(p["alg_bytes"] / p["launches"]),
-                               "ratio": round(p["hbm_bytes"] / p["alg_bytes"], 2)} for k, p in per.items()}}
+              "correction": "HBM bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads) + WRITE_SIZE x 1024",
+              "hbm_bytes_per_launch": round(hbm / n), "launches": n,
+              "variants": {k: {"launches": p["launches"], "hbm_bytes_per_launch": round(p["hbm_bytes"] / p["launches"])}
+                           for k, p in per.items()}}
+        if a.bench:
+            b = json.loads(Path(a.bench).read_text())
+            alg = b["roofline"]["algorithmic_bytes_per_launch"]
+            pm["alg_bytes_per_launch"] = alg
+            pm["ratio_hbm_to_alg"] = round(hbm / n / alg, 2)
         summary["pmc_gemm"] = pm
         (out_dir / "pmc_gemm_latest.json").write_text(json.dumps(pm, indent=1) + "\n")
     (out_dir / f"rocprof_{a.tag}.json").write_text(json.dumps(summary, indent=1) + "\n")
