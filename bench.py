@@ -199,7 +199,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded Pythia-2.8B-shaped weights, seeded single-token shuffled-label prompts)",
+        "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
         "config": {
             "workload": f"{args.model} CIE sweep {L}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
                         f"{args.kshot}-shot, T={T}",

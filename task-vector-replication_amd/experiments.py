@@ -322,3 +322,64 @@ def substitute_task(taskA: Pairs, taskB: Pairs, layer: int, function_token: str 
     a_to_b = sum(model.to_string(pt[i][0]) == ans[i][1] for i in range(n))
     b_to_a = sum(model.to_string(pt[i][1]) == ans[i][0] for i in range(n))
     return (num_contexts, a_hits, b_hits, a_to_b, b_to_a)
+
+
+# ------------------------------------------------------- batched FV evaluation
+def _fv_sites_topk(model: Model, contexts: Pairs, vectors: torch.Tensor, layer_vec: Sequence[Tuple[int, int]],
+                   topk: int):
+    """Top-k hits of every (prompt, (layer, vector)) pair in ONE sweep:
+    prompts ``x + ":"``, vector added to hook_attn_out[0, -1] at the layer
+    (scratch2.py:306-314 semantics).  Returns hits [len(layer_vec)]."""
+    seqs = [model.to_tokens(x + ":")[0].tolist() for x, _ in contexts]
+    firsts = [model.to_string(model.tokenizer.encode(y)[0]) for _, y in contexts]
+    n, m = len(seqs), len(layer_vec)
+    trace = model.trace(n, sum(len(s) for s in seqs))
+    model.forward_clean(seqs, trace=trace)
+    lv = np.asarray(layer_vec, dtype=np.int32).reshape(m, 2)
+    sites = make_sites(n * m)
+    sites["kind"] = _lib.SITE_ADD_ATTN_OUT_LASTPOS
+    sites["seq"] = np.repeat(np.arange(n), m)
+    sites["layer"] = np.tile(lv[:, 0], n)
+    sites["vec"] = np.tile(lv[:, 1], n)
+    vecs = vectors.to(model.device, torch.float32).reshape(-1, model.cfg.d_model).contiguous()
+    tops = []
+    for a, b in _chunks(len(sites), MAX_SITES_PER_LAUNCH):
+        tops.append(model.patch_sweep(trace, sites[a:b], vecs, topk=topk, want_prob=False)["topk"])
+    top = torch.cat(tops).view(n, m, topk).cpu().tolist()
+    hits = np.zeros(m, dtype=np.int64)
+    for i, first in enumerate(firsts):
+        for j in range(m):
+            hits[j] += first in [model.to_string(t) for t in top[i][j]]
+    return hits
+
+
+def check_accuracy_of_added_task_vector_by_layer(task_vector: torch.Tensor, contexts: Pairs, topk: int = 5,
+                                                 model: Model = None) -> List[float]:
+    """``check_accuracy_of_added_task_vector`` at every layer (one sweep)."""
+    L = model.cfg.n_layers
+    hits = _fv_sites_topk(model, contexts, task_vector.reshape(1, -1), [(l, 0) for l in range(L)], topk)
+    return [float(h) / len(contexts) for h in hits]
+
+
+def function_vector_head_count_grid(mean_head_activations: torch.Tensor, causal_indirect_effects: torch.Tensor,
+                                    contexts: Pairs, model: Model = None, heads_per_batch: int = 2,
+                                    number_of_batches: int = 64, topk: int = 5) -> torch.Tensor:
+    """The FV head-count grid of scratch2.py:411-425 as ONE batched sweep:
+    accuracy[i, j] of the function vector made of the top (j+1)*heads_per_batch
+    heads of layers <= i, added at layer i; entries the reference skips
+    ((j+1)*k >= (i+1)*n_heads) stay 0.  [n_layers, number_of_batches]."""
+    L, H = model.cfg.n_layers, model.cfg.n_heads
+    vecs, cells = [], []
+    for i in range(L):
+        for j in range(number_of_batches):
+            k = (j + 1) * heads_per_batch
+            if k < (i + 1) * H:
+                vecs.append(assemble_task_vector(mean_head_activations, causal_indirect_effects, i, k))
+                cells.append((i, j))
+    acc = torch.zeros(L, number_of_batches)
+    if not cells:
+        return acc
+    hits = _fv_sites_topk(model, contexts, torch.stack(vecs), [(i, v) for v, (i, _) in enumerate(cells)], topk)
+    for (i, j), h in zip(cells, hits):
+        acc[i, j] = float(h) / len(contexts)
+    return acc

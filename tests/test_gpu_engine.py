@@ -282,3 +282,30 @@ def test_pythia160m_shape_cie_subset(tokenizer):
     out = model.forward_clean(prompts, return_logits=True)
     for i, p in enumerate(prompts):
         assert rel_err(out["logits"][i], oracle.forward(torch.tensor([p]))[0, -1]) < 1e-4
+
+
+def test_batched_fv_helpers_match_reference_loops(tiny_model, tiny_oracle, mean_pair):
+    """check_accuracy_of_added_task_vector_by_layer and the head-count grid
+    (scratch2.py:411-425) = the reference's per-cell loops on the oracle."""
+    ours_mean, ref_mean = mean_pair
+    random.seed(3)
+    prompts, answers = tvr_amd.generate_shuffled_prompts(tvr_amd.tasks.letter_to_caps, tiny_model, 4, 4, ARROW)
+    cie = tvr_amd.calculate_average_causal_indirect_effect(ours_mean, prompts, answers, model=tiny_model)
+    cie_ref = R.calculate_average_causal_indirect_effect(ref_mean, prompts, answers, tiny_oracle)
+    ctx = tvr_amd.tasks.letter_to_caps[:30]
+    fv = tvr_amd.assemble_task_vector(ours_mean, cie, 1, 3) * 4
+    fv_ref = R.assemble_task_vector(ref_mean, cie_ref, 1, 3) * 4
+    by_layer = tvr_amd.experiments.check_accuracy_of_added_task_vector_by_layer(fv, ctx, 5, model=tiny_model)
+    assert by_layer == [R.check_accuracy_of_added_task_vector(fv_ref, l, ctx, 5, tiny_oracle)
+                        for l in range(tiny_oracle.cfg.n_layers)]
+    if torch.equal(torch.topk(cie.cpu().flatten(), 8).indices, torch.topk(cie_ref.flatten(), 8).indices):
+        grid = tvr_amd.experiments.function_vector_head_count_grid(ours_mean * 4, cie, ctx, model=tiny_model,
+                                                                   heads_per_batch=1, number_of_batches=6)
+        L, H = tiny_oracle.cfg.n_layers, tiny_oracle.cfg.n_heads
+        want = torch.zeros(L, 6)
+        for i in range(L):
+            for j in range(6):
+                if (j + 1) < (i + 1) * H:
+                    v = R.assemble_task_vector(ref_mean * 4, cie_ref, i, j + 1)
+                    want[i, j] = R.check_accuracy_of_added_task_vector(v, i, ctx, 5, tiny_oracle)
+        assert torch.equal(grid, want)
