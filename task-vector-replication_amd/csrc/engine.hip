@@ -364,7 +364,8 @@ int check_config(const tvr_config& c) {
     return fail(TVR_ERR_INVALID, "config: rotary_dim must be even and <= d_head");
   if (c.d_model % GEMM_BK != 0 || (c.d_model + c.d_mlp) % GEMM_BK != 0)
     return fail(TVR_ERR_UNSUPPORTED, "config: d_model and d_model + d_mlp must be multiples of 32");
-  if (c.d_head > 128) return fail(TVR_ERR_UNSUPPORTED, "config: d_head > 128");
+  if (c.d_head > 128 || c.d_head % 16 != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "config: d_head must be a multiple of 16 and <= 128");
   return TVR_OK;
 }
 
@@ -773,8 +774,12 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     const float* snap = trace->resid + (size_t)l * tstride;
     const float* zsnap = l > 0 ? trace->z + (size_t)(l - 1) * tstride : nullptr;
     const float* w2 = l > 0 ? m->layers[l - 1].w2 : nullptr;
+    const size_t zbytes = (size_t)maxT * c.d_head * sizeof(float);
+    if (zbytes > 64 * 1024)
+      TVR_HIP(hipFuncSetAttribute((const void*)entry_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)zbytes));
     hipLaunchKernelGGL(entry_kernel, dim3(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS),
-                       dim3(ENTRY_THREADS), 0, st, d_ents + k0, snap, zsnap, w2, m->K2, vectors,
+                       dim3(ENTRY_THREADS), zbytes, st, d_ents + k0, snap, zsnap, w2, m->K2, vectors,
                        a.resid, d, c.d_head);
     TVR_HIP(hipGetLastError());
     return TVR_OK;

@@ -105,29 +105,23 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
 
 // ---------------------------------------------------------------------------
 // Causal attention for ragged sequences with an optional clean K/V prefix.
-// grid = (n_seqs, n_heads), block = 256 (4 waves); each wave owns query rows
-// i = wave, wave+4, ...  K/V of every position live in LDS (rotary applied on
-// load); one score per lane per 64 keys.
+// grid = (n_seqs, n_heads), block = 256 (4 waves).  The block stages K and V
+// of every position (float4 loads; prefix from the clean trace's K/V, the rest
+// from this run), rotates K in LDS, then each wave owns query rows
+// q0+wave, q0+wave+4, ... with wave-private Q/P buffers: after the one staging
+// barrier no block-level barrier remains.  One score per lane per 64 keys,
+// wave-shuffle softmax, one output dim per lane.
 //   qkv  [rows][3d]: q at h*dh, k at d + h*dh, v at 2d + h*dh (pre-rotary)
 //   z    [rows][ldz]: written at h*dh  (attn.hook_z)
 constexpr int ATT_THREADS = 256;
 constexpr int ATT_MAX_T = 128;
 
-__device__ __forceinline__ void rotate_row(float* v, int pos, int rd,
-                                           const float* __restrict__ cos_t,
-                                           const float* __restrict__ sin_t,
-                                           int lane, int nlanes) {
-  // TL apply_rotary (rotate-half / non-adjacent pairs):
-  //   out[i] = x[i]*cos[i] - x[i+rd/2]*sin[i]         i <  rd/2
-  //   out[i] = x[i]*cos[i] + x[i-rd/2]*sin[i]         i >= rd/2
-  const int half = rd >> 1;
-  for (int i = lane; i < half; i += nlanes) {
-    const float x0 = v[i], x1 = v[i + half];
-    const float c0 = cos_t[pos * rd + i], s0 = sin_t[pos * rd + i];
-    const float c1 = cos_t[pos * rd + i + half], s1 = sin_t[pos * rd + i + half];
-    v[i] = x0 * c0 - x1 * s0;
-    v[i + half] = x1 * c1 + x0 * s1;
-  }
+// LDS ops of one wave retire in order; this only stops the compiler from
+// moving them across the point.
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+inline size_t attention_smem_bytes(int T, int dh) {
+  return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
 }
 
 __global__ void __launch_bounds__(ATT_THREADS)
@@ -143,82 +137,84 @@ attention_kernel(const float* __restrict__ qkv, int ldq,
   const int dhp = dh + 1;
   float* Ks = smem;                    // [T][dh+1]
   float* Vs = Ks + T * dhp;            // [T][dh+1]
-  float* Qs = Vs + T * dhp;            // [4][dh]
-  float* Ps = Qs + 4 * dh;             // [4][T]
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  float* Qs = Vs + T * dhp + wave * dh;          // wave-private [dh]
+  float* Ps = Vs + T * dhp + 4 * dh + wave * T;  // wave-private [T]
 
-  // K, V rows: prefix from the clean trace, the rest from this run
-  for (int e = t; e < T * dh; e += ATT_THREADS) {
-    const int j = e / dh, k = e - j * dh;
-    const float* src = (j < sd.p0)
-                           ? cache + (size_t)(sd.cache_row + j) * ldc
-                           : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
-    Ks[j * dhp + k] = src[d + h * dh + k];
-    Vs[j * dhp + k] = src[2 * d + h * dh + k];
+  // stage K, V (dh % 16 == 0: whole float4 per lane)
+  const int d4 = dh >> 2;
+  for (int e = t; e < T * d4; e += ATT_THREADS) {
+    const int j = e / d4, k = (e - j * d4) * 4;
+    const float* src = (j < sd.p0) ? cache + (size_t)(sd.cache_row + j) * ldc
+                                   : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
+    const float4 kv = *(const float4*)(src + d + h * dh + k);
+    const float4 vv = *(const float4*)(src + 2 * d + h * dh + k);
+    float* kr = Ks + j * dhp + k;
+    float* vr = Vs + j * dhp + k;
+    kr[0] = kv.x; kr[1] = kv.y; kr[2] = kv.z; kr[3] = kv.w;
+    vr[0] = vv.x; vr[1] = vv.y; vr[2] = vv.z; vr[3] = vv.w;
   }
   __syncthreads();
-  for (int j = wave; j < T; j += 4) rotate_row(Ks + j * dhp, j, rd, cos_t, sin_t, lane, 64);
+  // TL apply_rotary (rotate-half / non-adjacent pairs) on K, position j:
+  //   out[i] = x[i]*cos[i] - x[i+rd/2]*sin[i],  out[i+rd/2] = x[i+rd/2]*cos + x[i]*sin
+  const int half = rd >> 1;
+  for (int e = t; e < T * half; e += ATT_THREADS) {
+    const int j = e / half, i = e - j * half;
+    float* kr = Ks + j * dhp;
+    const float x0 = kr[i], x1 = kr[i + half];
+    kr[i] = x0 * cos_t[j * rd + i] - x1 * sin_t[j * rd + i];
+    kr[i + half] = x1 * cos_t[j * rd + i + half] + x0 * sin_t[j * rd + i + half];
+  }
   __syncthreads();
 
-  for (int ib = sd.q0; ib < sd.n; ib += 4) {
-    const int i = ib + wave;
-    const bool act = i < sd.n;
+  for (int i = sd.q0 + wave; i < sd.n; i += 4) {
     const int pos = sd.p0 + i;
-    float* q = Qs + wave * dh;
-    float* p = Ps + wave * T;
-    if (act) {
-      const float* qsrc = qkv + (size_t)(sd.row0 + i) * ldq + h * dh;
-      for (int k = lane; k < dh; k += 64) q[k] = qsrc[k];
+    const float* qsrc = qkv + (size_t)(sd.row0 + i) * ldq + h * dh;
+    for (int k = lane; k < dh; k += 64) {
+      float v = qsrc[k];
+      if (k < half) v = v * cos_t[pos * rd + k] - qsrc[k + half] * sin_t[pos * rd + k];
+      else if (k < rd) v = v * cos_t[pos * rd + k] + qsrc[k - half] * sin_t[pos * rd + k];
+      Qs[k] = v;
     }
-    __syncthreads();
-    if (act) rotate_row(q, pos, rd, cos_t, sin_t, lane, 64);
-    __syncthreads();
-    if (act) {
-      float sc[ATT_MAX_T / 64];
-      float mx = -INFINITY;
+    wave_lds_fence();
+    float sc[ATT_MAX_T / 64];
+    float mx = -INFINITY;
 #pragma unroll
-      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-        const int j = lane + 64 * u;
-        float s = -INFINITY;
-        if (j <= pos && j < T) {
-          const float* kr = Ks + j * dhp;
-          float a = 0.f;
-          for (int k = 0; k < dh; ++k) a += q[k] * kr[k];
-          s = a * inv_attn_scale;
-        }
-        sc[u] = s;
-        mx = fmaxf(mx, s);
-      }
-      mx = wave_max(mx);
-      float sum = 0.f;
-#pragma unroll
-      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-        const float e = (sc[u] == -INFINITY) ? 0.f : expf(sc[u] - mx);
-        sc[u] = e;
-        sum += e;
-      }
-      sum = wave_sum(sum);
-#pragma unroll
-      for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-        const int j = lane + 64 * u;
-        if (j < T) p[j] = sc[u] / sum;
-      }
-    }
-    __syncthreads();
-    if (act) {
-      float* zr = z + (size_t)(sd.row0 + i) * ldz + h * dh;
-      for (int k = lane; k < dh; k += 64) {
+    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+      const int j = lane + 64 * u;
+      float sv = -INFINITY;
+      if (j <= pos) {
+        const float* kr = Ks + j * dhp;
         float a = 0.f;
-        for (int j = 0; j <= pos; ++j) a += p[j] * Vs[j * dhp + k];
-        zr[k] = a;
+        for (int k = 0; k < dh; ++k) a += Qs[k] * kr[k];
+        sv = a * inv_attn_scale;
       }
+      sc[u] = sv;
+      mx = fmaxf(mx, sv);
     }
-    __syncthreads();
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+      const float ev = (sc[u] == -INFINITY) ? 0.f : expf(sc[u] - mx);
+      sc[u] = ev;
+      sum += ev;
+    }
+    sum = wave_sum(sum);
+#pragma unroll
+    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
+      const int j = lane + 64 * u;
+      if (j <= pos) Ps[j] = sc[u] / sum;
+    }
+    wave_lds_fence();
+    float* zr = z + (size_t)(sd.row0 + i) * ldz + h * dh;
+    for (int k = lane; k < dh; k += 64) {
+      float a = 0.f;
+      for (int j = 0; j <= pos; ++j) a += Ps[j] * Vs[j * dhp + k];
+      zr[k] = a;
+    }
+    wave_lds_fence();
   }
-}
-
-inline size_t attention_smem_bytes(int T, int dh) {
-  return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,40 +226,58 @@ inline size_t attention_smem_bytes(int T, int dh) {
 // REPLACE_HEAD (parallel residual): resid_pre[e] = clean resid_pre[e]
 //   + vec - z[e-1][:, h] @ W_O[e-1, h], at every position (scratch2.py:188).
 constexpr int ENTRY_THREADS = 256;
-constexpr int ENTRY_POS_CHUNK = 8;
+constexpr int ENTRY_POS_CHUNK = 16;
+constexpr int ENTRY_K_CHUNK = 16;
 
+// dynamic LDS: T x dh floats (the site's head slice of z; REPLACE_HEAD only)
 __global__ void __launch_bounds__(ENTRY_THREADS)
 entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
              const float* __restrict__ zsnap, const float* __restrict__ w2, int ldw2,
              const float* __restrict__ vectors, float* __restrict__ resid, int d, int dh) {
+  extern __shared__ __attribute__((aligned(16))) float zs[];
   const EntryDesc e = ents[blockIdx.x];
   const int c = blockIdx.y * ENTRY_THREADS + threadIdx.x;
-  if (c >= d) return;
   if (e.kind == 1) {  // TVR_SITE_REPLACE_HEAD_ALLPOS
+    for (int x = threadIdx.x; x < e.n * dh; x += ENTRY_THREADS) {
+      const int pos = x / dh, k = x - pos * dh;
+      zs[x] = zsnap[(size_t)(e.src_row + e.p0 + pos) * d + e.head * dh + k];
+    }
+    __syncthreads();
+    if (c >= d) return;
     const float* w = w2 + (size_t)c * ldw2 + e.head * dh;
     const float vc = vectors[(size_t)e.vec * d + c];
     for (int p0 = 0; p0 < e.n; p0 += ENTRY_POS_CHUNK) {
       float acc[ENTRY_POS_CHUNK];
 #pragma unroll
       for (int u = 0; u < ENTRY_POS_CHUNK; ++u) acc[u] = 0.f;
-      for (int k = 0; k < dh; ++k) {
-        const float wk = w[k];
+      for (int k0 = 0; k0 < dh; k0 += ENTRY_K_CHUNK) {
+        float wk[ENTRY_K_CHUNK];
+#pragma unroll
+        for (int q = 0; q < ENTRY_K_CHUNK; q += 4) {
+          const float4 v4 = *(const float4*)(w + k0 + q);  // dh % 16 == 0 (checked on the host)
+          wk[q] = v4.x; wk[q + 1] = v4.y; wk[q + 2] = v4.z; wk[q + 3] = v4.w;
+        }
 #pragma unroll
         for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
-          const int pos = e.p0 + p0 + u;
-          if (p0 + u < e.n)
-            acc[u] += zsnap[(size_t)(e.src_row + pos) * d + e.head * dh + k] * wk;
+          if (p0 + u < e.n) {
+            const float* zr = zs + (p0 + u) * dh + k0;
+#pragma unroll
+            for (int q = 0; q < ENTRY_K_CHUNK; ++q) acc[u] += zr[q] * wk[q];
+          }
         }
       }
 #pragma unroll
       for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
-        if (p0 + u >= e.n) break;
-        const int pos = e.p0 + p0 + u;
-        resid[(size_t)(e.row0 + p0 + u) * d + c] =
-            snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
+        if (p0 + u < e.n) {
+          const int pos = e.p0 + p0 + u;
+          resid[(size_t)(e.row0 + p0 + u) * d + c] = snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
+        }
       }
     }
-  } else if (e.kind == 2) {  // TVR_SITE_ADD_ATTN_OUT_LASTPOS
+    return;
+  }
+  if (c >= d) return;
+  if (e.kind == 2) {  // TVR_SITE_ADD_ATTN_OUT_LASTPOS
     for (int i = 0; i < e.n; ++i) {
       const int pos = e.p0 + i;
       resid[(size_t)(e.row0 + i) * d + c] =
