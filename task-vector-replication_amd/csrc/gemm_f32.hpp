@@ -69,6 +69,40 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// Shared epilogue of every GEMM kernel: wave tile of TM x TN 32x32
+// accumulators at (row_base, col_base).  32x32 C/D map (dtype-independent on
+// gfx950): col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue(const GemmEpi& ep, const f32x16 (&acc)[TM][TN], int M, int N,
+                                              int row_base, int col_base, int lr, int lh) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + j * 32 + lr;
+    if (col >= N) continue;
+    const float bcol = ep.bias ? ep.bias[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row_base + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= M) continue;
+        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
+        const float v = acc[i][j][r] + bcol;
+        if constexpr (EPI == EPI_BIAS) {
+          ep.out0[orow * ep.ld0 + col] = v;
+        } else if constexpr (EPI == EPI_SPLIT_GELU) {
+          if (col < ep.n_split)
+            ep.out0[orow * ep.ld0 + col] = v;
+          else
+            ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
+        } else {
+          ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
+        }
+      }
+    }
+  }
+}
+
 constexpr int GEMM_BK = 32;  // K granule the host must respect (every tile's BK divides it)
 constexpr int GEMM_GROUP_M = 8;
 
@@ -215,33 +249,7 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
     buf ^= 1;
   }
 
-  // Epilogue.  32x32 C/D map: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wc * (BN / TL::WN) + j * 32 + lr;
-    if (col >= N) continue;
-    const float bcol = ep.bias ? ep.bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wr * (BM / TL::WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= M) continue;
-        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
-        const float v = acc[i][j][r] + bcol;
-        if constexpr (EPI == EPI_BIAS) {
-          ep.out0[orow * ep.ld0 + col] = v;
-        } else if constexpr (EPI == EPI_SPLIT_GELU) {
-          if (col < ep.n_split)
-            ep.out0[orow * ep.ld0 + col] = v;
-          else
-            ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
-        } else {
-          ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
-        }
-      }
-    }
-  }
+  gemm_epilogue<EPI, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lr, lh);
   if (ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
