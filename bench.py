@@ -9,11 +9,18 @@ the prompt's first answer token (scratch2.py:171-197), i.e. 12,288 units per
 GPU per step.  Weights are seeded synthetic Pythia-2.8B (no checkpoints
 offline), fp32 like the reference (TransformerLens default dtype).
 
+GEMMs (95 % of the step) run on the fp32-accurate three-plane bf16 split
+(``--gemm x3bf16``, default: fp32 operands split exactly into 3 bf16 planes,
+6 products, fp32 accumulation; error at or below the fp32 MFMA GEMM's,
+tests/test_gpu_engine.py) or on ``v_mfma_f32_32x32x2_f32`` (``--gemm f32``).
+At N=1 an ``f32_leg`` re-times the same sweep on the fp32 MFMA path and
+reports the max CIE difference between the two paths.
+
 Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling — every rank
 sweeps its own prompts; the [L, H] CIE partial sums are all-reduced once per
 step (the mean over all prompts).  value = units of all ranks / max-rank time.
 
-Extra JSON objects: ``roofline`` (dominant kernel = fp32 MFMA GEMM, achieved
+Extra JSON objects: ``roofline`` (dominant kernel = the GEMM family, achieved
 from HIP events on the engine's launch stream), ``cpu_baseline`` (the CPU
 oracle running the reference's loop structure on a bounded sample, rank 0 at
 N=1 only).
@@ -33,6 +40,12 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "patched-forward prompts/sec, Pythia-2.8B layer×head CIE sweep, 1–8 GPUs"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec (155 measured)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (guide: "~2.5 PF dense")
+X3_PRODUCTS = 6                 # bf16 MFMA products per fp32-equivalent product
+PEAKS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3bf16": BF16_MFMA_PEAK_TFLOPS / X3_PRODUCTS}
+KERNELS = {"f32": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused epilogues)",
+           "x3bf16": "gemm_x3bf16_nt_kernel (3-plane bf16 split on v_mfma_f32_32x32x16_bf16, 6 products, "
+                     "fp32 accumulate; all three fused epilogues)"}
 
 
 def parse():
@@ -49,20 +62,27 @@ def parse():
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
+    ap.add_argument("--gemm", default="x3bf16", choices=("x3bf16", "f32"),
+                    help="matrix-core path of the GEMMs (both fp32-accurate; see module doc)")
+    ap.add_argument("--f32-leg", dest="f32_leg", action="store_true", default=True,
+                    help="N=1: also time the sweep on the fp32 MFMA GEMM and compare CIE")
+    ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks on one GPU")
     return ap.parse_args()
 
 
-def pmc_traffic():
+def pmc_traffic(family):
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary of
-    this bench command (profiles/pmc_gemm_latest.json, written by
-    tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE passes with
-    the gfx950 x2 FETCH_SIZE correction).  None if absent."""
-    p = ROOT / "profiles" / "pmc_gemm_latest.json"
+    this bench command on the same GEMM family (profiles/pmc_gemm_<family>.json,
+    written by tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE
+    passes with the gfx950 x2 FETCH_SIZE correction).  None if absent."""
+    p = ROOT / "profiles" / f"pmc_gemm_{family}.json"
     if not p.exists():
         return None, None
     d = json.loads(p.read_text())
+    if d.get("family") != family:
+        return None, None
     return d.get("hbm_bytes_per_launch"), f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
 
 
@@ -117,7 +137,7 @@ def main():
 
     cfg = tvr_amd.get_config(args.model)
     t0 = time.time()
-    model = tvr_amd.Model.from_pretrained(args.model, device=dev, seed=0)
+    model = tvr_amd.Model.from_pretrained(args.model, device=dev, seed=0, gemm=args.gemm)
     torch.cuda.synchronize()
     log(f"[rank {rank}] {args.model} synthetic weights on {dev} in {time.time() - t0:.1f}s")
 
@@ -148,23 +168,27 @@ def main():
             dist.all_reduce(cie)
         return cie
 
-    for _ in range(args.warmup):
-        step()
-    model.profile(True)  # HIP events around every GEMM launch of the timed region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cie = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+    def timed(warmup, steps, profile):
+        for _ in range(warmup):
+            step()
+        if profile:
+            model.profile(True)  # HIP events around every GEMM launch of the timed region
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            cie = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item(), cie
+
+    elapsed, cie = timed(args.warmup, args.steps, True)
     total_units = units_per_step * args.steps * world
     value = total_units / elapsed
 
@@ -173,7 +197,8 @@ def main():
     model.profile(False)
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src = pmc_traffic(args.gemm)
+    peak = PEAKS[args.gemm]
     T = len(prompts[0])
     L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
@@ -208,11 +233,15 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused epilogues)",
+            "kernel": KERNELS[args.gemm],
             "achieved": round(achieved, 2),
-            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "peak": round(peak, 1),
             "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "frac": round(achieved / peak, 4),
+            "flops_basis": "algorithmic fp32 2*M*N*K per launch / HIP-event launch time",
+            "peak_basis": ("fp32 MFMA dense peak" if args.gemm == "f32" else
+                           f"bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {X3_PRODUCTS} products "
+                           f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
             "traffic": traffic,
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": round(fam["bytes"] / max(fam["launches"], 1)),
@@ -228,6 +257,20 @@ def main():
             "extraction_prompts_per_s": round(n_ex / te, 1) if te else None,
         },
     }
+    out["config"]["gemm"] = args.gemm
+    if world == 1 and args.f32_leg and args.gemm != "f32":
+        model.set_gemm("f32")
+        el32, cie32 = timed(1, max(1, min(args.steps, 2)), True)
+        st32 = model.profile_stats()["all"]
+        model.profile(False)
+        model.set_gemm(args.gemm)
+        out["f32_leg"] = {
+            "gemm": "f32", "steps": max(1, min(args.steps, 2)),
+            "value": round(units_per_step * max(1, min(args.steps, 2)) / el32, 2),
+            "gemm_tflops": round(st32["flops"] / (st32["ms"] * 1e-3) / 1e12, 2),
+            "max_abs_cie_diff_vs_f32": float((cie - cie32).abs().max()),
+            "max_abs_cie": float(cie32.abs().max()),
+        }
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cfg, prompts, answers, mean)
     if rank == 0:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 1
+#define TVR_ABI_VERSION 2
 
 enum tvr_status {
   TVR_OK = 0,
@@ -116,6 +116,19 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed /*[V][d]*/,
                      const float* b_unembed /*[V]*/, tvr_model** out);
 int tvr_model_destroy(tvr_model* model);
 
+/* Matrix-core path of the model's GEMMs (every other op is fp32 regardless).
+ *   TVR_GEMM_F32     v_mfma_f32_32x32x2_f32 on the fp32 weights (default)
+ *   TVR_GEMM_X3BF16  fp32-accurate 3-plane bf16 split on v_mfma_f32_32x32x16_bf16:
+ *                    each operand x = x0+x1+x2 (bf16 planes, 24 significand bits),
+ *                    six cross products accumulated in fp32.  Measured error is
+ *                    at or below the fp32 MFMA GEMM's;
+ *                    the weight planes (6 B/param) are built on the device once.
+ * TransformerLens runs its matmuls in fp32 (scratch2.py:26 loads the default
+ * dtype); both modes meet that.  Synchronises `stream`. */
+enum tvr_gemm_mode { TVR_GEMM_F32 = 0, TVR_GEMM_X3BF16 = 1 };
+int tvr_model_set_gemm(tvr_model* model, int32_t mode, void* stream);
+int32_t tvr_model_get_gemm(const tvr_model* model);
+
 /* Clean-run trace: every layer's hook_resid_pre, attn.hook_z and the K/V
  * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */
 int tvr_trace_create(tvr_model* model, int32_t max_seqs, int32_t max_tokens,
@@ -168,6 +181,13 @@ int tvr_project_heads(tvr_model* model, const float* zsum /*[L][d]*/,
 int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw,
                  const float* bias, float* C, int32_t ldc, int32_t M,
                  int32_t N, int32_t K, void* stream);
+/* Split W [n] fp32 into 3 bf16 planes out [3][n] (uint16 storage). */
+int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream);
+/* tvr_gemm_f32 on the 3-plane operand: W planes [3][.][ldw] with plane
+ * stride wps elements (as tvr_split_planes writes them, wps = n). */
+int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
+                    size_t wps, const float* bias, float* C, int32_t ldc,
+                    int32_t M, int32_t N, int32_t K, void* stream);
 /* TransformerLens LayerNormPre over rows: (x - mean) / sqrt(var + eps) */
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
                   int32_t rows, int32_t d, float eps, void* stream);
@@ -187,7 +207,8 @@ typedef struct tvr_kernel_stats {
 int tvr_profile_enable(tvr_model* model, int32_t on);
 int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);
 
-/* Bytes of engine workspace currently held by the model (diagnostics). */
+/* Bytes of engine workspace currently held by the model (diagnostics);
+ * the X3BF16 weight planes are not included (6 B per GEMM weight). */
 size_t tvr_workspace_bytes(const tvr_model* model);
 
 #ifdef __cplusplus

@@ -56,6 +56,11 @@ class CKernelStats(ctypes.Structure):
 GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
+ABI_VERSION = 2  # include/tvr.h TVR_ABI_VERSION
+
+# include/tvr.h enum tvr_gemm_mode
+GEMM_MODES = {"f32": 0, "x3bf16": 1}
+
 SIGNATURES = {
     "tvr_version": (ctypes.c_char_p, []),
     "tvr_abi_version": (ctypes.c_int32, []),
@@ -82,6 +87,12 @@ SIGNATURES = {
     "tvr_lnpre_f32": (ctypes.c_int, [c_f32p, ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]),
     "tvr_workspace_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tvr_model_set_gemm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    "tvr_model_get_gemm": (ctypes.c_int32, [ctypes.c_void_p]),
+    "tvr_split_planes": (ctypes.c_int, [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "tvr_gemm_x3bf16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                       ctypes.c_size_t, c_f32p, c_f32p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
 }
@@ -108,7 +119,7 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.tvr_abi_version() != 1:
+    if lib.tvr_abi_version() != ABI_VERSION:
         raise EngineError("libtvr ABI mismatch")
     if path is None:
         _LIB = lib

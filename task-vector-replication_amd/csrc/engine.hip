@@ -19,6 +19,7 @@
 
 #include "tvr.h"
 #include "gemm_f32.hpp"
+#include "gemm_x3bf16.hpp"
 #include "kernels.hpp"
 
 using namespace tvr;
@@ -69,6 +70,15 @@ struct Staging {
   int next = 0;
 };
 
+// A GEMM weight operand: the fp32 matrix and, in TVR_GEMM_X3BF16 mode, its
+// three bf16 planes ([3][N][K], plane stride wps elements).
+struct MatW {
+  const float* f = nullptr;
+  const uint16_t* x = nullptr;
+  size_t wps = 0;
+  MatW rows(size_t elems) const { return {f + elems, x ? x + elems : nullptr, wps}; }
+};
+
 }  // namespace
 
 struct tvr_model {
@@ -82,6 +92,11 @@ struct tvr_model {
   float* rot_cos = nullptr;
   float* rot_sin = nullptr;
   const float** d_w2s = nullptr;
+  // GEMM operands (x planes set by tvr_model_set_gemm)
+  int gemm_mode = TVR_GEMM_F32;
+  uint16_t* planes = nullptr;
+  std::vector<MatW> w1, w2;
+  MatW wu;
   char* ws = nullptr;
   size_t ws_bytes = 0;
   Staging staging;
@@ -184,11 +199,11 @@ hipEvent_t prof_event(tvr_model* m) {
   return e;
 }
 
-int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M, int N,
+int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M, int N,
                 int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr) {
   if (M <= 0 || N <= 0) return TVR_OK;
-  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0)
-    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (K=" +
+  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || (W.x && ldw % 8 != 0))
+    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes; K=" +
                                          std::to_string(K) + ")");
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (m && m->prof) {
@@ -199,24 +214,30 @@ int launch_gemm(int epi, const float* A, int lda, const float* W, int ldw, int M
   const bool large = gemm_use_large(M, N);
 #define TVR_GEMM_LAUNCH(E, TL)                                                                  \
   hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
-                     st, A, lda, W, ldw, M, N, K, ep)
-  switch (epi) {
-    case EPI_BIAS:
-      if (large) TVR_GEMM_LAUNCH(EPI_BIAS, TileLarge); else TVR_GEMM_LAUNCH(EPI_BIAS, TileSmall);
-      break;
-    case EPI_SPLIT_GELU:
-      if (large) TVR_GEMM_LAUNCH(EPI_SPLIT_GELU, TileLarge); else TVR_GEMM_LAUNCH(EPI_SPLIT_GELU, TileSmall);
-      break;
-    default:
-      if (large) TVR_GEMM_LAUNCH(EPI_RESID, TileLarge); else TVR_GEMM_LAUNCH(EPI_RESID, TileSmall);
-      break;
+                     st, A, lda, W.f, ldw, M, N, K, ep)
+#define TVR_X3_LAUNCH(E, TL)                                                                      \
+  hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
+                     0, st, A, lda, W.x, ldw, W.wps, M, N, K, ep)
+#define TVR_GEMM_PICK(E)                                    \
+  if (W.x) {                                                \
+    if (large) TVR_X3_LAUNCH(E, X3Large); else TVR_X3_LAUNCH(E, X3Small);         \
+  } else {                                                  \
+    if (large) TVR_GEMM_LAUNCH(E, TileLarge); else TVR_GEMM_LAUNCH(E, TileSmall); \
   }
+  switch (epi) {
+    case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
+    case EPI_SPLIT_GELU: TVR_GEMM_PICK(EPI_SPLIT_GELU); break;
+    default: TVR_GEMM_PICK(EPI_RESID); break;
+  }
+#undef TVR_GEMM_PICK
+#undef TVR_X3_LAUNCH
 #undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
+    const double wbytes = W.x ? 6.0 : 4.0;  // W read once per launch: fp32, or 3 bf16 planes
     m->prof_recs.push_back({ev0, ev1, epi, 2.0 * M * N * (double)K,
-                            4.0 * ((double)M * K + (double)N * K + (double)M * N)});
+                            4.0 * ((double)M * K + (double)M * N) + wbytes * N * (double)K});
   }
   return TVR_OK;
 }
@@ -273,7 +294,7 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   e1.out1 = a.a2 + d;
   e1.ld1 = m->K2;
   e1.n_split = 3 * d;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1, d, R, m->D1, d, e1, st, m));
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l], d, R, m->D1, d, e1, st, m));
   return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st);
 }
 
@@ -295,7 +316,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   kv.out0 = a.qkv + d;
   kv.ld0 = 3 * d;
   kv.n_split = 2 * d;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1 + (size_t)d * d, d, R, 2 * d, d, kv, st, m));
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l].rows((size_t)d * d), d, R, 2 * d, d, kv, st, m));
   GemmEpi e1{};  // all columns for the last rows, gathered and scattered in place
   e1.bias = w.b1;
   e1.out0 = a.qkv;
@@ -305,7 +326,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e1.n_split = 3 * d;
   e1.a_rows = d_last;
   e1.out_rows = d_last;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, w.w1, d, n_last, m->D1, d, e1, st, m));
+  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l], d, n_last, m->D1, d, e1, st, m));
   TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
@@ -316,7 +337,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e2.ldr = d;
   e2.a_rows = d_last;
   e2.out_rows = d_last;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, w.w2, m->K2, n_last, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
 }
 
 int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
@@ -328,7 +349,7 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
   e2.ld0 = d;
   e2.resid = a.resid;
   e2.ldr = d;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, w.w2, m->K2, R, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
 }
 
 // Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
@@ -345,7 +366,7 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
     e.bias = m->b_unembed;
     e.out0 = lg;
     e.ld0 = V;
-    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, m->w_unembed_t, d, cn, V, d, e, st, m));
+    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, m->wu, d, cn, V, d, e, st, m));
     hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
                        d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
                        out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
@@ -374,7 +395,7 @@ int check_config(const tvr_config& c) {
 // ===========================================================================
 extern "C" {
 
-const char* tvr_version(void) { return "tvr-mi355x 0.1.0 (gfx950, fp32 MFMA)"; }
+const char* tvr_version(void) { return "tvr-mi355x 0.2.0 (gfx950, fp32 MFMA | fp32-accurate 3xbf16 MFMA)"; }
 int32_t tvr_abi_version(void) { return TVR_ABI_VERSION; }
 const char* tvr_last_error(void) { return g_last_error.c_str(); }
 
@@ -394,6 +415,11 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_laye
   m->layers.assign(layers, layers + cfg->n_layers);
   m->w_unembed_t = w_unembed_t;
   m->b_unembed = b_unembed;
+  for (int l = 0; l < cfg->n_layers; ++l) {
+    m->w1.push_back({layers[l].w1, nullptr, 0});
+    m->w2.push_back({layers[l].w2, nullptr, 0});
+  }
+  m->wu = {w_unembed_t, nullptr, 0};
   // TL calculate_sin_cos_rotary: freq = base^(i / (rd/2)), repeated "(2 d)",
   // angle = pos / freq, all in fp32.
   const int rd = std::max(cfg->rotary_dim, 2), n_ctx = cfg->n_ctx;
@@ -429,6 +455,7 @@ int tvr_model_destroy(tvr_model* m) {
   if (m->rot_cos) (void)hipFree(m->rot_cos);
   if (m->rot_sin) (void)hipFree(m->rot_sin);
   if (m->d_w2s) (void)hipFree(m->d_w2s);
+  if (m->planes) (void)hipFree(m->planes);
   if (m->ws) (void)hipFree(m->ws);
   for (auto& r : m->prof_recs) {
     (void)hipEventDestroy(r.a);
@@ -444,6 +471,52 @@ int tvr_model_destroy(tvr_model* m) {
 }
 
 size_t tvr_workspace_bytes(const tvr_model* m) { return m ? m->ws_bytes : 0; }
+
+int32_t tvr_model_get_gemm(const tvr_model* m) { return m ? m->gemm_mode : -1; }
+
+int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
+  if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: null model");
+  if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16)
+    return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: unknown mode " + std::to_string(mode));
+  if (mode == m->gemm_mode) return TVR_OK;
+  const hipStream_t st = (hipStream_t)stream;
+  TVR_HIP(hipStreamSynchronize(st));
+  if (mode == TVR_GEMM_F32) {
+    for (auto& w : m->w1) w = {w.f, nullptr, 0};
+    for (auto& w : m->w2) w = {w.f, nullptr, 0};
+    m->wu = {m->wu.f, nullptr, 0};
+    if (m->planes) TVR_HIP(hipFree(m->planes));
+    m->planes = nullptr;
+    m->gemm_mode = mode;
+    return TVR_OK;
+  }
+  const tvr_config& c = m->cfg;
+  const size_t n1 = (size_t)m->D1 * c.d_model, n2 = (size_t)c.d_model * m->K2;
+  const size_t nu = (size_t)c.d_vocab * c.d_model;
+  const size_t total = 3 * ((n1 + n2) * c.n_layers + nu);
+  if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
+    m->planes = nullptr;
+    (void)hipGetLastError();
+    return fail(TVR_ERR_NOMEM, "tvr_model_set_gemm: weight planes (" + std::to_string(total * 2) +
+                                   " bytes) do not fit");
+  }
+  uint16_t* p = m->planes;
+  auto split = [&](MatW& w, size_t n) -> int {
+    hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
+    TVR_HIP(hipGetLastError());
+    w = {w.f, p, n};
+    p += 3 * n;
+    return TVR_OK;
+  };
+  for (int l = 0; l < c.n_layers; ++l) {
+    TVR_TRY(split(m->w1[l], n1));
+    TVR_TRY(split(m->w2[l], n2));
+  }
+  TVR_TRY(split(m->wu, nu));
+  TVR_HIP(hipStreamSynchronize(st));
+  m->gemm_mode = mode;
+  return TVR_OK;
+}
 
 int tvr_profile_enable(tvr_model* m, int32_t on) {
   if (!m) return fail(TVR_ERR_INVALID, "tvr_profile_enable: null model");
@@ -821,7 +894,26 @@ int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw, const
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, W, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, MatW{W, nullptr, 0}, ldw, M, N, K, e, (hipStream_t)stream);
+}
+
+int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream) {
+  if (!w || !out) return fail(TVR_ERR_INVALID, "tvr_split_planes: null argument");
+  if (n == 0) return TVR_OK;
+  hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, out, n);
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
+int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw, size_t wps,
+                    const float* bias, float* C, int32_t ldc, int32_t M, int32_t N, int32_t K, void* stream) {
+  if (!A || !W || !C || M < 0 || N < 0 || K <= 0 || wps < (size_t)ldw * (N > 0 ? N - 1 : 0) + K)
+    return fail(TVR_ERR_INVALID, "tvr_gemm_x3bf16: bad argument");
+  GemmEpi e{};
+  e.bias = bias;
+  e.out0 = C;
+  e.ld0 = ldc;
+  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, W, wps}, ldw, M, N, K, e, (hipStream_t)stream);
 }
 
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy, int32_t rows, int32_t d, float eps,

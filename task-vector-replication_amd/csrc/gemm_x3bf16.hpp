@@ -15,9 +15,13 @@
 //   * W is pre-split once at load time: 3 planes [N][K] bf16, plane stride
 //     `wps` elements.  A (activations) stays fp32 in HBM and is split while it
 //     is staged into LDS (each element once per block).
-//   * 256x256 block tile, BK = 16 (one MFMA k-group per plane), 8 waves of
+//   * BK = 16 (one MFMA k-group per plane).  256x256 block tile, 8 waves of
 //     128x64 (4 x 2 accumulators); LDS: 2 buffers x 2 operands x 3 planes x 256
 //     rows x 48 B (16 bf16 + 8 pad: conflict-free ds_read_b128) = 144 KB.
+//     A 128x128 / 4-wave variant covers small M (same 512-tile rule as f32).
+//   * Measured (profiles/gemm_x3_probe_r01.jsonl, M=90000): 211 TF/s of
+//     algorithmic fp32 work = 1.55x the fp32 MFMA GEMM, max error 2.8e-7 vs
+//     3.4e-7 of sum|a*w| (fp64 truth).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,21 +41,25 @@ __device__ __forceinline__ void split3(float x, __bf16& h0, __bf16& h1, __bf16& 
   h2 = (__bf16)(r1 - (float)h1);
 }
 
-struct X3Tile {
-  static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, BK = 16;
+template <int BM_, int BN_, int WM_, int WN_>
+struct X3TileT {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = 16;
   static constexpr int LDK = BK + 8;  // bf16 elements per LDS row (48 B)
   static constexpr int THREADS = WM * WN * 64;
   static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static constexpr int LOADS_A = BM * BK / 4 / THREADS;  // float4 of A per thread (2)
+  static constexpr int LOADS_A = BM * BK / 4 / THREADS;  // float4 of A per thread
   static constexpr int PLANE = BM * LDK;                 // bf16 elements per LDS plane
+  static_assert(BM == BN, "one LDS plane size for A and W");
   static_assert(BN * BK / 8 == THREADS, "one 16-B W chunk per thread per plane");
+  static_assert(LOADS_A * THREADS * 4 == BM * BK, "A tile covered by float4 loads");
 };
+using X3Large = X3TileT<256, 256, 2, 4>;  // 8 waves of 128x64, 144 KB LDS
+using X3Small = X3TileT<128, 128, 2, 2>;  // 4 waves of 64x64, 72 KB LDS (small M)
 
-template <int EPI>
-__global__ void __launch_bounds__(X3Tile::THREADS, 2)
+template <int EPI, class TL>
+__global__ void __launch_bounds__(TL::THREADS, 2)
 gemm_x3bf16_nt_kernel(const float* __restrict__ A, int lda, const uint16_t* __restrict__ W, int ldw,
                       size_t wps, int M, int N, int K, GemmEpi ep) {
-  using TL = X3Tile;
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN, NT = TL::THREADS;
   constexpr int BK = TL::BK, LDK = TL::LDK, PL = TL::PLANE;
   const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -188,8 +196,9 @@ __global__ void split_planes_kernel(const float* __restrict__ w, uint16_t* __res
   }
 }
 
+template <class TL>
 inline int gemm_x3_grid(int M, int N) {
-  return ((M + X3Tile::BM - 1) / X3Tile::BM) * ((N + X3Tile::BN - 1) / X3Tile::BN);
+  return ((M + TL::BM - 1) / TL::BM) * ((N + TL::BN - 1) / TL::BN);
 }
 
 }  // namespace tvr

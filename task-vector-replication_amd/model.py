@@ -76,7 +76,7 @@ class Trace:
 
 class Model(TokenizerMixin):
     def __init__(self, cfg: PythiaConfig, weights: EngineWeights, tokenizer=None,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, gemm: str = "x3bf16"):
         self._h = None
         self._lib = _lib.load()
         dev = torch.device(device) if device is not None else weights.w_embed.device
@@ -104,15 +104,17 @@ class Model(TokenizerMixin):
                 "tvr_model_create")
         self._h = h
         self._trace_cache: Optional[Trace] = None
+        self.set_gemm(gemm)
 
     # ------------------------------------------------------------------ build
     @classmethod
     def from_pretrained(cls, name: str, device="cuda", seed: int = 0, checkpoint: Optional[str] = None,
                         tokenizer_path: Optional[str] = None, std: float = 0.02, ln_std: float = 0.1,
-                        cfg: Optional[PythiaConfig] = None) -> "Model":
+                        cfg: Optional[PythiaConfig] = None, gemm: str = "x3bf16") -> "Model":
         """``HookedTransformer.from_pretrained`` without a network: the named
         Pythia shape with seeded synthetic weights (generated on the device), or
-        a local HF-layout safetensors ``checkpoint``."""
+        a local HF-layout safetensors ``checkpoint``.  ``gemm`` picks the
+        matrix-core path (see :meth:`set_gemm`)."""
         cfg = cfg if cfg is not None else get_config(name)
         dev = torch.device(device)
         if checkpoint:
@@ -120,11 +122,25 @@ class Model(TokenizerMixin):
         else:
             w = synth_engine_weights(cfg, seed=seed, device=dev, std=std, ln_std=ln_std)
         tok = HFTokenizer(tokenizer_path) if tokenizer_path else None
-        return cls(cfg, w, tokenizer=tok, device=dev)
+        return cls(cfg, w, tokenizer=tok, device=dev, gemm=gemm)
 
     @classmethod
-    def from_hf_state_dict(cls, cfg: PythiaConfig, sd, device="cuda", tokenizer=None) -> "Model":
-        return cls(cfg, process_to_engine(cfg, sd, device=torch.device(device)), tokenizer, device)
+    def from_hf_state_dict(cls, cfg: PythiaConfig, sd, device="cuda", tokenizer=None,
+                           gemm: str = "x3bf16") -> "Model":
+        return cls(cfg, process_to_engine(cfg, sd, device=torch.device(device)), tokenizer, device, gemm)
+
+    def set_gemm(self, mode: str) -> None:
+        """Matrix-core path of every GEMM (include/tvr.h ``tvr_model_set_gemm``):
+        ``"x3bf16"`` (default) — fp32-accurate three-plane bf16 split on the bf16
+        MFMA (error at or below the fp32 MFMA GEMM's, 1.55x faster; costs 6 B per
+        weight for the planes); ``"f32"`` — ``v_mfma_f32_32x32x2_f32`` on the fp32
+        weights.  Everything outside the GEMMs is fp32 in both."""
+        if mode not in _lib.GEMM_MODES:
+            raise ValueError(f"gemm mode must be one of {sorted(_lib.GEMM_MODES)}, got {mode!r}")
+        with torch.cuda.device(self.device):
+            _lib.check(self._lib.tvr_model_set_gemm(self._h, _lib.GEMM_MODES[mode], self._stream()),
+                       "tvr_model_set_gemm")
+        self.gemm = mode
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -65,8 +65,16 @@ def tiny_oracle64(tiny_cfg, tiny_sd, tokenizer):
     return make_oracle(tiny_cfg, tiny_sd, tokenizer, torch.float64)
 
 
-@pytest.fixture(scope="session")
-def tiny_model(tiny_cfg, tiny_sd, tokenizer):
+GEMM_MODES = ("x3bf16", "f32")
+
+
+@pytest.fixture(scope="session", params=GEMM_MODES)
+def tiny_model(request, tiny_cfg, tiny_sd, tokenizer):
+    """The engine on the tiny model, once per GEMM path (every parity test
+    runs against both matrix-core paths at the same tolerance)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    return tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer)
+    m = tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer,
+                                         gemm=request.param)
+    assert m._lib.tvr_model_get_gemm(m._h) == tvr_amd._lib.GEMM_MODES[request.param]
+    return m

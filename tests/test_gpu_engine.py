@@ -49,6 +49,32 @@ def test_gemm_f32_matches_torch(M, N, K):
     assert (t32 - ref).abs().max().item() <= 2 * bound
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 1, 32), (37, 130, 64), (128, 128, 32), (300, 257, 320),
+                                   (1000, 2560, 2560), (129, 50304, 64),
+                                   (4096, 8192, 256), (3001, 17920, 96), (1025, 50304, 64)])
+def test_gemm_x3bf16_matches_torch(M, N, K):
+    """The 3-plane bf16 split GEMM meets the SAME bound as the fp32 MFMA GEMM."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 1e-3  # planes keep their own exponents
+    b = torch.randn(N, generator=g)
+    C = torch.empty(M, N, device="cuda")
+    lib = tvr_amd._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    planes = torch.empty(3, N, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_split_planes(Wd.data_ptr(), planes.data_ptr(), N * K, st), "split")
+    # the planes sum back to W exactly
+    bf = planes.view(torch.bfloat16).double()
+    assert torch.equal(bf.sum(0), Wd.double())
+    tvr_amd._lib.check(lib.tvr_gemm_x3bf16(Ad.data_ptr(), K, planes.data_ptr(), K, N * K, bd.data_ptr(),
+                                           C.data_ptr(), N, M, N, K, st), "gemm_x3")
+    ref = A.double() @ W.double().T + b.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    bound = 4e-7 * (A.double().abs() @ W.double().abs().T).max().item() + 1e-6
+    assert err <= bound, (err, bound)
+
+
 def test_lnpre_matches_torch():
     x = torch.randn(77, 2560, device="cuda") * 3 + 1
     y = torch.empty_like(x)
@@ -263,13 +289,14 @@ def test_patch_sweep_site_kinds_against_hooks(tiny_model, tiny_oracle):
 
 
 @pytest.mark.slow
-def test_pythia160m_shape_cie_subset(tokenizer):
+@pytest.mark.parametrize("gemm", ["x3bf16", "f32"])
+def test_pythia160m_shape_cie_subset(tokenizer, gemm):
     """Pythia-160m shape (d 768, 12 heads, d_head 64): clean logits and a CIE
     stripe (3 layers x 12 heads, 2 prompts) against the fp32 oracle."""
     from conftest import make_oracle
     cfg = tvr_amd.get_config("pythia-160m")
     sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
-    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda")
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", gemm=gemm)
     oracle = make_oracle(cfg, sd, model.tokenizer)
     prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, 2, 4, seed=1234)
     g = torch.Generator().manual_seed(0)

@@ -55,7 +55,7 @@ int main() {
                          dim3(TileLarge::THREADS), 0, 0, A, s.K, W, s.K, s.M, s.N, s.K, e1);
     };
     auto run_x3 = [&]() {
-      hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS>), dim3(gemm_x3_grid(s.M, s.N)), dim3(X3Tile::THREADS), 0, 0,
+      hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS, X3Large>), dim3(gemm_x3_grid<X3Large>(s.M, s.N)), dim3(X3Large::THREADS), 0, 0,
                          A, s.K, Wp, s.K, (size_t)s.N * s.K, s.M, s.N, s.K, e2);
     };
     hipEvent_t a, b;

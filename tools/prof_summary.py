@@ -10,7 +10,8 @@
   reports half the bytes of 16-B/lane streaming reads) + WRITE_SIZE x 1024,
   next to the launch's algorithmic bytes (A + W + C, fp32).
 Writes profiles/rocprof_<tag>.json, profiles/kernel_stats_<tag>.csv and
-profiles/pmc_gemm_latest.json (read by bench.py for roofline.traffic).
+profiles/pmc_gemm_<family>.json (read by bench.py for roofline.traffic;
+family = f32 | x3bf16, the GEMM kernel the profiled command ran).
 """
 import argparse
 import csv
@@ -34,10 +35,15 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
+FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16"}
+
+
 def gemm_variant(name):
-    if "gemm_f32_nt_kernel<" not in name:
-        return None
-    return name.split("gemm_f32_nt_kernel<")[1][0]
+    """(family, epilogue variant) of a GEMM kernel name, or None."""
+    for k, fam in FAMILIES.items():
+        if k + "<" in name:
+            return fam, name.split(k + "<")[1][0]
+    return None
 
 
 def pmc(d):
@@ -66,25 +72,34 @@ def main():
                         "total_ms": round(int(r["TotalDurationNs"]) / 1e6, 3),
                         "avg_ms": round(float(r["AverageNs"]) / 1e6, 4), "pct": round(float(r["Percentage"]), 2)})
     summary = {"command": a.cmd, "kernels": kernels[:20]}
-    gemm = [k for k in kernels if "gemm_f32_nt_kernel" in k["kernel"]]
+    gemm = [k for k in kernels if any(f in k["kernel"] for f in FAMILIES)]
     tot_calls = sum(k["calls"] for k in gemm)
     summary["gemm_family"] = {"calls": tot_calls, "total_ms": round(sum(k["total_ms"] for k in gemm), 3),
                               "avg_ms": round(sum(k["total_ms"] for k in gemm) / max(tot_calls, 1), 4)}
     if a.fetch and a.write:
         f, w = pmc(a.fetch), pmc(a.write)
-        per = {}
-        for rf, rw in zip(f, w):
-            v = gemm_variant(rf["Kernel_Name"])
-            if v is None:
-                continue
-            assert rf["Dispatch_Id"] == rw["Dispatch_Id"] or True
+        # the two passes are separate runs of the same deterministic command:
+        # pair the i-th GEMM dispatch of one with the i-th of the other
+        fg = [r for r in f if gemm_variant(r["Kernel_Name"])]
+        wg = [r for r in w if gemm_variant(r["Kernel_Name"])]
+        if len(fg) != len(wg):
+            raise SystemExit(f"PMC passes saw {len(fg)} vs {len(wg)} GEMM dispatches")
+        per, fams = {}, set()
+        for rf, rw in zip(fg, wg):
+            fam, v = gemm_variant(rf["Kernel_Name"])
+            if gemm_variant(rw["Kernel_Name"]) != (fam, v):
+                raise SystemExit("PMC passes disagree on the GEMM dispatch order")
+            fams.add(fam)
             hbm = 2.0 * float(rf["Counter_Value"]) * 1024 + float(rw["Counter_Value"]) * 1024
             p = per.setdefault(VARIANTS[v], {"launches": 0, "hbm_bytes": 0.0})
             p["launches"] += 1
             p["hbm_bytes"] += hbm
         n = sum(p["launches"] for p in per.values())
         hbm = sum(p["hbm_bytes"] for p in per.values())
-        pm = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}",
+        if len(fams) != 1:
+            raise SystemExit(f"profiled command ran GEMM families {sorted(fams)}; profile one at a time")
+        fam = fams.pop()
+        pm = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}", "family": fam,
               "correction": "HBM bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads) + WRITE_SIZE x 1024",
               "hbm_bytes_per_launch": round(hbm / n), "launches": n,
               "variants": {k: {"launches": p["launches"], "hbm_bytes_per_launch": round(p["hbm_bytes"] / p["launches"])}
@@ -95,7 +110,7 @@ def main():
             pm["alg_bytes_per_launch"] = alg
             pm["ratio_hbm_to_alg"] = round(hbm / n / alg, 2)
         summary["pmc_gemm"] = pm
-        (out_dir / "pmc_gemm_latest.json").write_text(json.dumps(pm, indent=1) + "\n")
+        (out_dir / f"pmc_gemm_{fam}.json").write_text(json.dumps(pm, indent=1) + "\n")
     (out_dir / f"rocprof_{a.tag}.json").write_text(json.dumps(summary, indent=1) + "\n")
     print(json.dumps(summary, indent=1)[:3000])
 
