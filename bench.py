@@ -72,7 +72,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(family):
+def pmc_traffic(family, workload):
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary of
     this bench command on the same GEMM family (profiles/pmc_gemm_<family>.json,
     written by tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE
@@ -81,8 +81,8 @@ def pmc_traffic(family):
     if not p.exists():
         return None, None
     d = json.loads(p.read_text())
-    if d.get("family") != family:
-        return None, None
+    if d.get("family") != family or d.get("workload") != workload:
+        return None, None  # counters of another kernel or workload do not apply
     return d.get("hbm_bytes_per_launch"), f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
 
 
@@ -197,9 +197,11 @@ def main():
     model.profile(False)
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(args.gemm)
-    peak = PEAKS[args.gemm]
     T = len(prompts[0])
+    workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
+                f"{args.kshot}-shot, T={T}")
+    traffic, traffic_src = pmc_traffic(args.gemm, workload)
+    peak = PEAKS[args.gemm]
     L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
     # F_alg(site at layer l) = (L-1-l)(2 P_l T + 2 T(T+1) d) + 2 d V
@@ -226,8 +228,7 @@ def main():
         "dtype": "f32",
         "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
         "config": {
-            "workload": f"{args.model} CIE sweep {L}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
-                        f"{args.kshot}-shot, T={T}",
+            "workload": workload,
             "sites_per_step_per_gpu": units_per_step,
             "parallelism": f"prompt-sharded x{world}, weights replicated, 1 all-reduce of [L,H] per step",
         },

@@ -25,7 +25,7 @@ VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout"}
 
 
 def one(d, pattern):
-    hits = glob.glob(str(Path(d) / pattern))
+    hits = glob.glob(str(Path(d) / "**" / pattern), recursive=True)
     if not hits:
         raise SystemExit(f"no {pattern} under {d}")
     return hits[0]
@@ -60,9 +60,10 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--bench", help="bench.py JSON of the same command (algorithmic bytes per launch)")
-    ap.add_argument("--cmd", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline")
+    ap.add_argument("--cmd", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg")
+    ap.add_argument("--out", default=str(ROOT / "profiles"), help="summary directory")
     a = ap.parse_args()
-    out_dir = ROOT / "profiles"
+    out_dir = Path(a.out)
     out_dir.mkdir(exist_ok=True)
     stats_csv = one(a.stats, "*kernel_stats.csv")
     shutil.copy(stats_csv, out_dir / f"kernel_stats_{a.tag}.csv")
@@ -108,6 +109,7 @@ def main():
             b = json.loads(Path(a.bench).read_text())
             alg = b["roofline"]["algorithmic_bytes_per_launch"]
             pm["alg_bytes_per_launch"] = alg
+            pm["workload"] = b["config"]["workload"]
             pm["ratio_hbm_to_alg"] = round(hbm / n / alg, 2)
         summary["pmc_gemm"] = pm
         (out_dir / f"pmc_gemm_{fam}.json").write_text(json.dumps(pm, indent=1) + "\n")
