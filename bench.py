@@ -9,12 +9,15 @@ the prompt's first answer token (scratch2.py:171-197), i.e. 12,288 units per
 GPU per step.  Weights are seeded synthetic Pythia-2.8B (no checkpoints
 offline), fp32 like the reference (TransformerLens default dtype).
 
-GEMMs (95 % of the step) run on the fp32-accurate three-plane bf16 split
-(``--gemm x3bf16``, default: fp32 operands split exactly into 3 bf16 planes,
-6 products, fp32 accumulation; error at or below the fp32 MFMA GEMM's,
-tests/test_gpu_engine.py) or on ``v_mfma_f32_32x32x2_f32`` (``--gemm f32``).
-At N=1 an ``f32_leg`` re-times the same sweep on the fp32 MFMA path and
-reports the max CIE difference between the two paths.
+GEMMs (95 % of the step) run on the fp32-accurate two-plane fp16 split
+(``--gemm x2f16``, default: fp32 operands split into 2 power-of-two-scaled
+fp16 planes, 3 products on v_mfma_f32_32x32x16_f16, fp32 accumulation — the
+fp16 form of 3xTF32), the three-plane bf16 split (``--gemm x3bf16``: 6
+products) or ``v_mfma_f32_32x32x2_f32`` (``--gemm f32``).  Both splits measure
+at or below the fp32 MFMA GEMM's error against fp64 (tests/test_gpu_engine.py,
+profiles/gemm_split_probe_r01.jsonl).  At N=1 an ``f32_leg`` re-times the same
+sweep on the fp32 MFMA path and reports the max CIE difference between the
+two paths.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling — every rank
 sweeps its own prompts; the [L, H] CIE partial sums are all-reduced once per
@@ -41,11 +44,15 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "patched-forward prompts/sec, Pythia-2.8B layer×head CIE sweep, 1–8 GPUs"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 spec (155 measured)
 BF16_MFMA_PEAK_TFLOPS = 2516.6  # 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz (guide: "~2.5 PF dense")
-X3_PRODUCTS = 6                 # bf16 MFMA products per fp32-equivalent product
-PEAKS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3bf16": BF16_MFMA_PEAK_TFLOPS / X3_PRODUCTS}
+# 16-bit MFMA products per fp32-equivalent product (fp16 and bf16 MFMA run at one rate)
+PRODUCTS = {"x3bf16": 6, "x2f16": 3}
+PEAKS = {"f32": FP32_MFMA_PEAK_TFLOPS, "x3bf16": BF16_MFMA_PEAK_TFLOPS / PRODUCTS["x3bf16"],
+         "x2f16": BF16_MFMA_PEAK_TFLOPS / PRODUCTS["x2f16"]}
 KERNELS = {"f32": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused epilogues)",
            "x3bf16": "gemm_x3bf16_nt_kernel (3-plane bf16 split on v_mfma_f32_32x32x16_bf16, 6 products, "
-                     "fp32 accumulate; all three fused epilogues)"}
+                     "fp32 accumulate; all three fused epilogues)",
+           "x2f16": "gemm_x2f16_nt_kernel (2-plane fp16 split on v_mfma_f32_32x32x16_f16, 3 products, "
+                    "fp32 accumulate; all three fused epilogues)"}
 
 
 def parse():
@@ -62,8 +69,8 @@ def parse():
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
-    ap.add_argument("--gemm", default="x3bf16", choices=("x3bf16", "f32"),
-                    help="matrix-core path of the GEMMs (both fp32-accurate; see module doc)")
+    ap.add_argument("--gemm", default="x2f16", choices=("x2f16", "x3bf16", "f32"),
+                    help="matrix-core path of the GEMMs (all fp32-accurate; see module doc)")
     ap.add_argument("--f32-leg", dest="f32_leg", action="store_true", default=True,
                     help="N=1: also time the sweep on the fp32 MFMA GEMM and compare CIE")
     ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
@@ -241,7 +248,7 @@ def main():
             "frac": round(achieved / peak, 4),
             "flops_basis": "algorithmic fp32 2*M*N*K per launch / HIP-event launch time",
             "peak_basis": ("fp32 MFMA dense peak" if args.gemm == "f32" else
-                           f"bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {X3_PRODUCTS} products "
+                           f"fp16/bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {PRODUCTS[args.gemm]} products "
                            f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
             "traffic": traffic,
             "traffic_source": traffic_src,

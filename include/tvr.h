@@ -35,14 +35,15 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 2
+#define TVR_ABI_VERSION 3
 
 enum tvr_status {
   TVR_OK = 0,
   TVR_ERR_INVALID = -1,     /* bad argument / shape (reference: ValueError) */
   TVR_ERR_HIP = -2,         /* HIP runtime failure */
   TVR_ERR_NOMEM = -3,       /* device allocation failed */
-  TVR_ERR_UNSUPPORTED = -4  /* shape outside what the kernels handle */
+  TVR_ERR_UNSUPPORTED = -4, /* shape outside what the kernels handle */
+  TVR_ERR_RANGE = -5        /* a GEMM input exceeded the TVR_GEMM_X2F16 range */
 };
 
 /* Patch-site kinds: the declarative replacement for TransformerLens hooks. */
@@ -117,17 +118,29 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed /*[V][d]*/,
 int tvr_model_destroy(tvr_model* model);
 
 /* Matrix-core path of the model's GEMMs (every other op is fp32 regardless).
- *   TVR_GEMM_F32     v_mfma_f32_32x32x2_f32 on the fp32 weights (default)
+ *   TVR_GEMM_F32     v_mfma_f32_32x32x2_f32 on the fp32 weights
  *   TVR_GEMM_X3BF16  fp32-accurate 3-plane bf16 split on v_mfma_f32_32x32x16_bf16:
  *                    each operand x = x0+x1+x2 (bf16 planes, 24 significand bits),
- *                    six cross products accumulated in fp32.  Measured error is
- *                    at or below the fp32 MFMA GEMM's;
- *                    the weight planes (6 B/param) are built on the device once.
- * TransformerLens runs its matmuls in fp32 (scratch2.py:26 loads the default
- * dtype); both modes meet that.  Synchronises `stream`. */
-enum tvr_gemm_mode { TVR_GEMM_F32 = 0, TVR_GEMM_X3BF16 = 1 };
+ *                    six cross products accumulated in fp32; weight planes 6 B/param
+ *   TVR_GEMM_X2F16   fp32-accurate 2-plane fp16 split on v_mfma_f32_32x32x16_f16
+ *                    (the fp16 form of 3xTF32): x = x0+x1 (2 x 11 significand
+ *                    bits, power-of-two scaled into fp16 range), three cross
+ *                    products accumulated in fp32; weight planes 4 B/param.
+ *                    GEMM inputs must satisfy |a| < 4095 (LayerNorm outputs,
+ *                    attention mixes and GELU outputs of any Pythia do); a
+ *                    launch that sees a larger one is reported by
+ *                    tvr_model_range_status.
+ * Measured errors of both split modes against fp64 are at or below the fp32
+ * MFMA GEMM's.  TransformerLens runs its matmuls in fp32
+ * (scratch2.py:26 loads the default dtype); all three modes meet that.  The
+ * planes are built on the device once.  Synchronises `stream`. */
+enum tvr_gemm_mode { TVR_GEMM_F32 = 0, TVR_GEMM_X3BF16 = 1, TVR_GEMM_X2F16 = 2 };
 int tvr_model_set_gemm(tvr_model* model, int32_t mode, void* stream);
 int32_t tvr_model_get_gemm(const tvr_model* model);
+/* TVR_OK, or TVR_ERR_RANGE if an X2F16 GEMM enqueued since the last call saw
+ * an input outside its range (its results are then not fp32-accurate and must
+ * be discarded).  Synchronises `stream`; clears the flag. */
+int tvr_model_range_status(tvr_model* model, void* stream);
 
 /* Clean-run trace: every layer's hook_resid_pre, attn.hook_z and the K/V
  * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */
@@ -188,6 +201,16 @@ int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream);
 int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
                     size_t wps, const float* bias, float* C, int32_t ldc,
                     int32_t M, int32_t N, int32_t K, void* stream);
+/* Split W [n] fp32 into 2 fp16 planes out [2][n] of w * scale (uint16
+ * storage); scale is a power of two (X2F16 mode picks 2^(15 - ceil log2 max|W|)). */
+int tvr_split_planes_f16(const float* w, float scale, uint16_t* out, size_t n, void* stream);
+/* tvr_gemm_f32 on the 2-plane fp16 operand: W planes [2][.][ldw] (plane stride
+ * wps) built with scale w_scale.  *range_flag (device, may be NULL) is or-ed
+ * with 1 if |A| reaches the split's range limit. */
+int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
+                   size_t wps, float w_scale, const float* bias, float* C,
+                   int32_t ldc, int32_t M, int32_t N, int32_t K,
+                   uint32_t* range_flag, void* stream);
 /* TransformerLens LayerNormPre over rows: (x - mean) / sqrt(var + eps) */
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
                   int32_t rows, int32_t d, float eps, void* stream);
@@ -208,7 +231,8 @@ int tvr_profile_enable(tvr_model* model, int32_t on);
 int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);
- * the X3BF16 weight planes are not included (6 B per GEMM weight). */
+ * the split-mode weight planes are not included (X3BF16 6 B, X2F16 4 B per
+ * GEMM weight). */
 size_t tvr_workspace_bytes(const tvr_model* model);
 
 #ifdef __cplusplus

@@ -19,6 +19,7 @@ TVR_ERR_INVALID = -1
 TVR_ERR_HIP = -2
 TVR_ERR_NOMEM = -3
 TVR_ERR_UNSUPPORTED = -4
+TVR_ERR_RANGE = -5
 
 # enum tvr_trace_hook
 TRACE_RESID_PRE = 0
@@ -56,10 +57,10 @@ class CKernelStats(ctypes.Structure):
 GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 2  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 3  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
-GEMM_MODES = {"f32": 0, "x3bf16": 1}
+GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2}
 
 SIGNATURES = {
     "tvr_version": (ctypes.c_char_p, []),
@@ -93,6 +94,13 @@ SIGNATURES = {
     "tvr_gemm_x3bf16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                        ctypes.c_size_t, c_f32p, c_f32p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    "tvr_model_range_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tvr_split_planes_f16": (ctypes.c_int, [c_f32p, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_void_p]),
+    "tvr_gemm_x2f16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                      ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
 }

@@ -19,6 +19,7 @@
 
 #include "tvr.h"
 #include "gemm_f32.hpp"
+#include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
 #include "kernels.hpp"
 
@@ -70,13 +71,18 @@ struct Staging {
   int next = 0;
 };
 
-// A GEMM weight operand: the fp32 matrix and, in TVR_GEMM_X3BF16 mode, its
-// three bf16 planes ([3][N][K], plane stride wps elements).
+// A GEMM weight operand: the fp32 matrix and, in a split mode, its planes
+// (plane stride wps elements): TVR_GEMM_X3BF16 three bf16 planes in x,
+// TVR_GEMM_X2F16 two fp16 planes of w * wscale in h.
 struct MatW {
   const float* f = nullptr;
   const uint16_t* x = nullptr;
+  const uint16_t* h = nullptr;
   size_t wps = 0;
-  MatW rows(size_t elems) const { return {f + elems, x ? x + elems : nullptr, wps}; }
+  float wscale = 1.0f;
+  MatW rows(size_t elems) const {
+    return {f + elems, x ? x + elems : nullptr, h ? h + elems : nullptr, wps, wscale};
+  }
 };
 
 }  // namespace
@@ -95,6 +101,7 @@ struct tvr_model {
   // GEMM operands (x planes set by tvr_model_set_gemm)
   int gemm_mode = TVR_GEMM_F32;
   uint16_t* planes = nullptr;
+  unsigned* range_flag = nullptr;  // device word: X2F16 input out of range since the last status read
   std::vector<MatW> w1, w2;
   MatW wu;
   char* ws = nullptr;
@@ -200,9 +207,10 @@ hipEvent_t prof_event(tvr_model* m) {
 }
 
 int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M, int N,
-                int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr) {
+                int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr,
+                unsigned* range_flag = nullptr) {
   if (M <= 0 || N <= 0) return TVR_OK;
-  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || (W.x && ldw % 8 != 0))
+  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0))
     return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes; K=" +
                                          std::to_string(K) + ")");
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -218,8 +226,15 @@ int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M,
 #define TVR_X3_LAUNCH(E, TL)                                                                      \
   hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
                      0, st, A, lda, W.x, ldw, W.wps, M, N, K, ep)
+  unsigned* flag = m ? m->range_flag : range_flag;
+  const float acc_scale = 1.0f / (W.wscale * X2_ASCALE);
+#define TVR_X2_LAUNCH(E, TL)                                                                         \
+  hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
+                     st, A, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
 #define TVR_GEMM_PICK(E)                                    \
-  if (W.x) {                                                \
+  if (W.h) {                                                \
+    if (large) TVR_X2_LAUNCH(E, X2Large); else TVR_X2_LAUNCH(E, X2Small);         \
+  } else if (W.x) {                                         \
     if (large) TVR_X3_LAUNCH(E, X3Large); else TVR_X3_LAUNCH(E, X3Small);         \
   } else {                                                  \
     if (large) TVR_GEMM_LAUNCH(E, TileLarge); else TVR_GEMM_LAUNCH(E, TileSmall); \
@@ -231,11 +246,12 @@ int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M,
   }
 #undef TVR_GEMM_PICK
 #undef TVR_X3_LAUNCH
+#undef TVR_X2_LAUNCH
 #undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
-    const double wbytes = W.x ? 6.0 : 4.0;  // W read once per launch: fp32, or 3 bf16 planes
+    const double wbytes = W.x ? 6.0 : 4.0;  // W read once per launch: fp32, 3 bf16 or 2 fp16 planes
     m->prof_recs.push_back({ev0, ev1, epi, 2.0 * M * N * (double)K,
                             4.0 * ((double)M * K + (double)M * N) + wbytes * N * (double)K});
   }
@@ -395,7 +411,9 @@ int check_config(const tvr_config& c) {
 // ===========================================================================
 extern "C" {
 
-const char* tvr_version(void) { return "tvr-mi355x 0.2.0 (gfx950, fp32 MFMA | fp32-accurate 3xbf16 MFMA)"; }
+const char* tvr_version(void) {
+  return "tvr-mi355x 0.3.0 (gfx950, fp32 MFMA | fp32-accurate 3-plane bf16 / 2-plane fp16 split MFMA)";
+}
 int32_t tvr_abi_version(void) { return TVR_ABI_VERSION; }
 const char* tvr_last_error(void) { return g_last_error.c_str(); }
 
@@ -416,10 +434,10 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_laye
   m->w_unembed_t = w_unembed_t;
   m->b_unembed = b_unembed;
   for (int l = 0; l < cfg->n_layers; ++l) {
-    m->w1.push_back({layers[l].w1, nullptr, 0});
-    m->w2.push_back({layers[l].w2, nullptr, 0});
+    m->w1.push_back(MatW{layers[l].w1});
+    m->w2.push_back(MatW{layers[l].w2});
   }
-  m->wu = {w_unembed_t, nullptr, 0};
+  m->wu = MatW{w_unembed_t};
   // TL calculate_sin_cos_rotary: freq = base^(i / (rd/2)), repeated "(2 d)",
   // angle = pos / freq, all in fp32.
   const int rd = std::max(cfg->rotary_dim, 2), n_ctx = cfg->n_ctx;
@@ -438,6 +456,8 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_laye
   hipError_t e = hipMalloc(&m->rot_cos, hc.size() * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&m->rot_sin, hs.size() * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&m->d_w2s, w2s.size() * sizeof(float*));
+  if (e == hipSuccess) e = hipMalloc(&m->range_flag, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(m->range_flag, 0, sizeof(unsigned));
   if (e == hipSuccess) e = hipMemcpy(m->rot_cos, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(m->rot_sin, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(m->d_w2s, w2s.data(), w2s.size() * sizeof(float*), hipMemcpyHostToDevice);
@@ -456,6 +476,7 @@ int tvr_model_destroy(tvr_model* m) {
   if (m->rot_sin) (void)hipFree(m->rot_sin);
   if (m->d_w2s) (void)hipFree(m->d_w2s);
   if (m->planes) (void)hipFree(m->planes);
+  if (m->range_flag) (void)hipFree(m->range_flag);
   if (m->ws) (void)hipFree(m->ws);
   for (auto& r : m->prof_recs) {
     (void)hipEventDestroy(r.a);
@@ -476,46 +497,93 @@ int32_t tvr_model_get_gemm(const tvr_model* m) { return m ? m->gemm_mode : -1; }
 
 int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: null model");
-  if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16)
+  if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16 && mode != TVR_GEMM_X2F16)
     return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: unknown mode " + std::to_string(mode));
   if (mode == m->gemm_mode) return TVR_OK;
   const hipStream_t st = (hipStream_t)stream;
   TVR_HIP(hipStreamSynchronize(st));
-  if (mode == TVR_GEMM_F32) {
-    for (auto& w : m->w1) w = {w.f, nullptr, 0};
-    for (auto& w : m->w2) w = {w.f, nullptr, 0};
-    m->wu = {m->wu.f, nullptr, 0};
-    if (m->planes) TVR_HIP(hipFree(m->planes));
-    m->planes = nullptr;
-    m->gemm_mode = mode;
-    return TVR_OK;
-  }
+  // back to plain fp32 operands first (frees the previous mode's planes)
+  for (auto& w : m->w1) w = MatW{w.f};
+  for (auto& w : m->w2) w = MatW{w.f};
+  m->wu = MatW{m->wu.f};
+  if (m->planes) TVR_HIP(hipFree(m->planes));
+  m->planes = nullptr;
+  m->gemm_mode = TVR_GEMM_F32;
+  if (mode == TVR_GEMM_F32) return TVR_OK;
+
   const tvr_config& c = m->cfg;
+  const int L = c.n_layers;
   const size_t n1 = (size_t)m->D1 * c.d_model, n2 = (size_t)c.d_model * m->K2;
   const size_t nu = (size_t)c.d_vocab * c.d_model;
-  const size_t total = 3 * ((n1 + n2) * c.n_layers + nu);
+  const int np = mode == TVR_GEMM_X3BF16 ? 3 : 2;
+  const size_t total = np * ((n1 + n2) * L + nu);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
     (void)hipGetLastError();
     return fail(TVR_ERR_NOMEM, "tvr_model_set_gemm: weight planes (" + std::to_string(total * 2) +
                                    " bytes) do not fit");
   }
-  uint16_t* p = m->planes;
-  auto split = [&](MatW& w, size_t n) -> int {
-    hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
-    TVR_HIP(hipGetLastError());
-    w = {w.f, p, n};
-    p += 3 * n;
-    return TVR_OK;
-  };
-  for (int l = 0; l < c.n_layers; ++l) {
-    TVR_TRY(split(m->w1[l], n1));
-    TVR_TRY(split(m->w2[l], n2));
+  // every GEMM weight matrix in order: w1[0], w2[0], ..., w1[L-1], w2[L-1], wu
+  std::vector<MatW*> mats;
+  std::vector<size_t> sizes;
+  for (int l = 0; l < L; ++l) {
+    mats.push_back(&m->w1[l]); sizes.push_back(n1);
+    mats.push_back(&m->w2[l]); sizes.push_back(n2);
   }
-  TVR_TRY(split(m->wu, nu));
+  mats.push_back(&m->wu); sizes.push_back(nu);
+  std::vector<float> scale(mats.size(), 1.0f);
+  if (mode == TVR_GEMM_X2F16) {
+    // one power-of-two scale per matrix from its largest magnitude
+    unsigned* d_max = nullptr;
+    TVR_HIP(hipMalloc(&d_max, mats.size() * sizeof(unsigned)));
+    std::vector<unsigned> h_max(mats.size(), 0);
+    hipError_t e = hipMemsetAsync(d_max, 0, mats.size() * sizeof(unsigned), st);
+    for (size_t i = 0; i < mats.size() && e == hipSuccess; ++i) {
+      hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, mats[i]->f, sizes[i], d_max + i);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h_max.data(), d_max, mats.size() * sizeof(unsigned),
+                                            hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d_max);
+    if (e != hipSuccess) return fail(TVR_ERR_HIP, std::string("tvr_model_set_gemm: ") + hipGetErrorString(e));
+    for (size_t i = 0; i < mats.size(); ++i) {
+      float v;
+      std::memcpy(&v, &h_max[i], sizeof(v));
+      scale[i] = x2_weight_scale(v);
+    }
+  }
+  uint16_t* p = m->planes;
+  for (size_t i = 0; i < mats.size(); ++i) {
+    MatW& w = *mats[i];
+    const size_t n = sizes[i];
+    if (mode == TVR_GEMM_X3BF16) {
+      hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
+      w = MatW{w.f, p, nullptr, n, 1.0f};
+    } else {
+      hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, st, w.f, scale[i], p, n);
+      w = MatW{w.f, nullptr, p, n, scale[i]};
+    }
+    TVR_HIP(hipGetLastError());
+    p += np * n;
+  }
+  TVR_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(unsigned), st));
   TVR_HIP(hipStreamSynchronize(st));
   m->gemm_mode = mode;
   return TVR_OK;
+}
+
+int tvr_model_range_status(tvr_model* m, void* stream) {
+  if (!m) return fail(TVR_ERR_INVALID, "tvr_model_range_status: null model");
+  const hipStream_t st = (hipStream_t)stream;
+  unsigned h = 0;
+  TVR_HIP(hipMemcpyAsync(&h, m->range_flag, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  TVR_HIP(hipStreamSynchronize(st));
+  if (h == 0) return TVR_OK;
+  TVR_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(unsigned), st));
+  TVR_HIP(hipStreamSynchronize(st));
+  return fail(TVR_ERR_RANGE, "a GEMM input reached |a| >= 4095, outside the fp16-split (X2F16) range; "
+                             "results since the last check are not fp32-accurate: use gemm mode x3bf16 or f32");
 }
 
 int tvr_profile_enable(tvr_model* m, int32_t on) {
@@ -894,7 +962,7 @@ int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw, const
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, MatW{W, nullptr, 0}, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, MatW{W}, ldw, M, N, K, e, (hipStream_t)stream);
 }
 
 int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream) {
@@ -913,7 +981,29 @@ int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, W, wps}, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, W, nullptr, wps, 1.0f}, ldw, M, N, K, e, (hipStream_t)stream);
+}
+
+int tvr_split_planes_f16(const float* w, float scale, uint16_t* out, size_t n, void* stream) {
+  if (!w || !out) return fail(TVR_ERR_INVALID, "tvr_split_planes_f16: null argument");
+  if (n == 0) return TVR_OK;
+  hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, scale, out, n);
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
+int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw, size_t wps, float w_scale,
+                   const float* bias, float* C, int32_t ldc, int32_t M, int32_t N, int32_t K,
+                   uint32_t* range_flag, void* stream) {
+  if (!A || !W || !C || M < 0 || N < 0 || K <= 0 || !(w_scale > 0.0f) ||
+      wps < (size_t)ldw * (N > 0 ? N - 1 : 0) + K)
+    return fail(TVR_ERR_INVALID, "tvr_gemm_x2f16: bad argument");
+  GemmEpi e{};
+  e.bias = bias;
+  e.out0 = C;
+  e.ld0 = ldc;
+  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
+                     (hipStream_t)stream, nullptr, range_flag);
 }
 
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy, int32_t rows, int32_t d, float eps,

@@ -74,9 +74,14 @@ class Trace:
             self._h = None
 
 
+# Matrix-core path of the GEMMs (Model.set_gemm): the fp32-accurate 2-plane
+# fp16 split is the fastest path whose error is at or below the fp32 MFMA's.
+DEFAULT_GEMM = "x2f16"
+
+
 class Model(TokenizerMixin):
     def __init__(self, cfg: PythiaConfig, weights: EngineWeights, tokenizer=None,
-                 device: Optional[torch.device] = None, gemm: str = "x3bf16"):
+                 device: Optional[torch.device] = None, gemm: str = DEFAULT_GEMM):
         self._h = None
         self._lib = _lib.load()
         dev = torch.device(device) if device is not None else weights.w_embed.device
@@ -110,7 +115,7 @@ class Model(TokenizerMixin):
     @classmethod
     def from_pretrained(cls, name: str, device="cuda", seed: int = 0, checkpoint: Optional[str] = None,
                         tokenizer_path: Optional[str] = None, std: float = 0.02, ln_std: float = 0.1,
-                        cfg: Optional[PythiaConfig] = None, gemm: str = "x3bf16") -> "Model":
+                        cfg: Optional[PythiaConfig] = None, gemm: str = DEFAULT_GEMM) -> "Model":
         """``HookedTransformer.from_pretrained`` without a network: the named
         Pythia shape with seeded synthetic weights (generated on the device), or
         a local HF-layout safetensors ``checkpoint``.  ``gemm`` picks the
@@ -126,15 +131,19 @@ class Model(TokenizerMixin):
 
     @classmethod
     def from_hf_state_dict(cls, cfg: PythiaConfig, sd, device="cuda", tokenizer=None,
-                           gemm: str = "x3bf16") -> "Model":
+                           gemm: str = DEFAULT_GEMM) -> "Model":
         return cls(cfg, process_to_engine(cfg, sd, device=torch.device(device)), tokenizer, device, gemm)
 
     def set_gemm(self, mode: str) -> None:
         """Matrix-core path of every GEMM (include/tvr.h ``tvr_model_set_gemm``):
-        ``"x3bf16"`` (default) — fp32-accurate three-plane bf16 split on the bf16
-        MFMA (error at or below the fp32 MFMA GEMM's, 1.55x faster; costs 6 B per
-        weight for the planes); ``"f32"`` — ``v_mfma_f32_32x32x2_f32`` on the fp32
-        weights.  Everything outside the GEMMs is fp32 in both."""
+        ``"x2f16"`` (default) — fp32-accurate two-plane fp16 split (the fp16 form
+        of 3xTF32: three products on the fp16 MFMA, 4 B per weight for the
+        planes; inputs must stay below 4095 in magnitude, checked on the device
+        after every engine call); ``"x3bf16"`` — fp32-accurate three-plane bf16
+        split (six products, 6 B per weight, no range limit); ``"f32"`` —
+        ``v_mfma_f32_32x32x2_f32`` on the fp32 weights.  Both splits measure at
+        or below the fp32 MFMA GEMM's error against fp64.
+        Everything outside the GEMMs is fp32 in all three."""
         if mode not in _lib.GEMM_MODES:
             raise ValueError(f"gemm mode must be one of {sorted(_lib.GEMM_MODES)}, got {mode!r}")
         with torch.cuda.device(self.device):
@@ -152,6 +161,12 @@ class Model(TokenizerMixin):
     # ------------------------------------------------------------- internals
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _check_range(self, what: str) -> None:
+        """x2f16 only: fail loudly if a GEMM input left the fp16 split's range
+        (synchronises the stream)."""
+        if self.gemm == "x2f16":
+            _lib.check(self._lib.tvr_model_range_status(self._h, self._stream()), what)
 
     def trace(self, n_seqs: int, n_tokens: int) -> Trace:
         """A trace with at least this capacity (reused across calls)."""
@@ -199,6 +214,7 @@ class Model(TokenizerMixin):
             tg.ctypes.data if tg is not None else None,
             _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits), _lib.ptr(zsum), self._stream())
         _lib.check(rc, "tvr_forward_clean")
+        self._check_range("tvr_forward_clean")
         if trace is not None:
             trace.seq_lens = lens.tolist()
             trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
@@ -234,6 +250,7 @@ class Model(TokenizerMixin):
                                        _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits),
                                        self._stream())
         _lib.check(rc, "tvr_patch_sweep")
+        self._check_range("tvr_patch_sweep")
         out = {}
         if prob is not None:
             out["prob"] = prob

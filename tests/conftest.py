@@ -65,13 +65,13 @@ def tiny_oracle64(tiny_cfg, tiny_sd, tokenizer):
     return make_oracle(tiny_cfg, tiny_sd, tokenizer, torch.float64)
 
 
-GEMM_MODES = ("x3bf16", "f32")
+GEMM_MODES = ("x2f16", "x3bf16", "f32")
 
 
 @pytest.fixture(scope="session", params=GEMM_MODES)
 def tiny_model(request, tiny_cfg, tiny_sd, tokenizer):
     """The engine on the tiny model, once per GEMM path (every parity test
-    runs against both matrix-core paths at the same tolerance)."""
+    runs against every matrix-core path at the same tolerance)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     m = tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer,

@@ -75,6 +75,58 @@ def test_gemm_x3bf16_matches_torch(M, N, K):
     assert err <= bound, (err, bound)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 1, 32), (37, 130, 64), (128, 128, 32), (300, 257, 320),
+                                   (1000, 2560, 2560), (129, 50304, 64),
+                                   (4096, 8192, 256), (3001, 17920, 96), (1025, 50304, 64)])
+def test_gemm_x2f16_matches_torch(M, N, K):
+    """The 2-plane fp16 split GEMM meets the SAME bound as the fp32 MFMA GEMM,
+    with weights far from fp16's natural range (the power-of-two scale)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g)
+    A[:, ::7] *= 1e-4  # tiny inputs: the residual plane's subnormal range
+    W = torch.randn(N, K, generator=g) * 1e-3
+    b = torch.randn(N, generator=g)
+    C = torch.empty(M, N, device="cuda")
+    lib = tvr_amd._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    e = int(np.frexp(W.abs().max().item())[1])
+    scale = float(2.0 ** (15 - e))
+    planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_split_planes_f16(Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
+    # the planes sum back to W * scale within 2^-22 relative, or half the fp16
+    # subnormal spacing (2^-25) where the residual plane is subnormal
+    hp = planes.view(torch.float16).double()
+    ws = Wd.double() * scale
+    assert ((hp.sum(0) - ws).abs() <= 2.0 ** -22 * ws.abs() + 2.0 ** -25).all()
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    tvr_amd._lib.check(lib.tvr_gemm_x2f16(Ad.data_ptr(), K, planes.data_ptr(), K, N * K, scale, bd.data_ptr(),
+                                          C.data_ptr(), N, M, N, K, flag.data_ptr(), st), "gemm_x2")
+    ref = A.double() @ W.double().T + b.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    bound = 4e-7 * (A.double().abs() @ W.double().abs().T).max().item() + 1e-6
+    assert err <= bound, (err, bound)
+    assert flag.item() == 0
+
+
+def test_gemm_x2f16_range_flag():
+    """An input at the split's range limit (|a| >= 4095) is reported, not hidden."""
+    M, N, K = 64, 64, 64
+    lib = tvr_amd._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    A = torch.randn(M, K, device="cuda")
+    W = torch.randn(N, K, device="cuda") * 0.02
+    planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_split_planes_f16(W.data_ptr(), 2.0 ** 16, planes.data_ptr(), N * K, st), "split")
+    C = torch.empty(M, N, device="cuda")
+    for big, want in ((4000.0, 0), (4100.0, 1)):
+        A[5, 9] = big
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        tvr_amd._lib.check(lib.tvr_gemm_x2f16(A.data_ptr(), K, planes.data_ptr(), K, N * K, 2.0 ** 16, None,
+                                              C.data_ptr(), N, M, N, K, flag.data_ptr(), st), "gemm_x2")
+        assert flag.item() == want, big
+
+
 def test_lnpre_matches_torch():
     x = torch.randn(77, 2560, device="cuda") * 3 + 1
     y = torch.empty_like(x)
@@ -289,7 +341,7 @@ def test_patch_sweep_site_kinds_against_hooks(tiny_model, tiny_oracle):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("gemm", ["x3bf16", "f32"])
+@pytest.mark.parametrize("gemm", ["x2f16", "x3bf16", "f32"])
 def test_pythia160m_shape_cie_subset(tokenizer, gemm):
     """Pythia-160m shape (d 768, 12 heads, d_head 64): clean logits and a CIE
     stripe (3 layers x 12 heads, 2 prompts) against the fp32 oracle."""

@@ -1,0 +1,156 @@
+// gemm_split_probe.hip — speed, in-kernel clock and accuracy of the three GEMM
+// paths (fp32 MFMA, 3-plane bf16 split, 2-plane fp16 split) at the engine's
+// real shapes, each checked against an fp64 reference on sampled rows.
+//   hipcc --offload-arch=gfx950 -O3 -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
+//   tools/gemm_split_probe [f32|x3|x2 ...]      (default: all three)
+// A is drawn N(0,1) (a LayerNorm output) or GELU(3 N(0,1)) (the MLP-out input:
+// many tiny values, which exercises the fp16 residual plane's range).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../task-vector-replication_amd/csrc/gemm_x2f16.hpp"
+#include "../task-vector-replication_amd/csrc/gemm_x3bf16.hpp"
+
+using namespace tvr;
+
+__global__ void fill_normal(float* p, size_t n, unsigned seed, float scale, int gelu) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    unsigned x = (unsigned)(i * 2654435761u) ^ seed, y = (unsigned)((i >> 32) * 40503u) ^ (seed * 7919u) ^ (unsigned)i;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15; y ^= x; y ^= y >> 13; y *= 0x5bd1e995u; y ^= y >> 15;
+    const float u1 = ((x & 0xffffff) + 0.5f) / 16777216.0f, u2 = ((y & 0xffffff) + 0.5f) / 16777216.0f;
+    const float v = scale * sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
+    p[i] = gelu ? gelu_erf(v) : v;
+  }
+}
+
+__global__ void ref64(const float* A, const float* W, const int* rows, int nr, int N, int K, double* out, double* mag) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nr * N) return;
+  const int r = idx / N, n = idx % N;
+  const float* a = A + (size_t)rows[r] * K;
+  const float* w = W + (size_t)n * K;
+  double s = 0, m = 0;
+  for (int k = 0; k < K; ++k) { s += (double)a[k] * (double)w[k]; m += fabs((double)a[k] * (double)w[k]); }
+  out[idx] = s;
+  mag[idx] = m;
+}
+
+int main(int argc, char** argv) {
+  std::vector<std::string> paths;
+  for (int i = 1; i < argc; ++i) paths.push_back(argv[i]);
+  if (paths.empty()) paths = {"f32", "x3", "x2"};
+  struct Shape { const char* name; int M, N, K; int gelu; };
+  std::vector<Shape> shapes = {{"qkv_mlpin", 90000, 17920, 2560, 0}, {"o_mlpout", 90000, 2560, 12800, 1}};
+  for (auto& s : shapes) {
+    float *A, *W, *C;
+    uint16_t *W3, *W2;
+    unsigned *flag, *wmax_bits;
+    unsigned long long* stamps;
+    const int maxgrid = gemm_grid<TileSmall>(s.M, s.N);
+    hipMalloc(&A, sizeof(float) * (size_t)s.M * s.K);
+    hipMalloc(&W, sizeof(float) * (size_t)s.N * s.K);
+    hipMalloc(&W3, sizeof(uint16_t) * 3 * (size_t)s.N * s.K);
+    hipMalloc(&W2, sizeof(uint16_t) * 2 * (size_t)s.N * s.K);
+    hipMalloc(&C, sizeof(float) * (size_t)s.M * s.N);
+    hipMalloc(&flag, 8);
+    hipMalloc(&wmax_bits, 8);
+    hipMalloc(&stamps, sizeof(unsigned long long) * 2 * maxgrid);
+    hipMemset(flag, 0, 8);
+    hipMemset(wmax_bits, 0, 8);
+    hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, A, (size_t)s.M * s.K, 11u, s.gelu ? 3.0f : 1.0f, s.gelu);
+    hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, W, (size_t)s.N * s.K, 29u, 0.02f, 0);
+    hipLaunchKernelGGL(split_planes_kernel, dim3(8192), dim3(256), 0, 0, W, W3, (size_t)s.N * s.K);
+    hipLaunchKernelGGL(absmax_kernel, dim3(2048), dim3(256), 0, 0, W, (size_t)s.N * s.K, wmax_bits);
+    unsigned wb = 0;
+    hipMemcpy(&wb, wmax_bits, 4, hipMemcpyDeviceToHost);
+    float wmax;
+    std::memcpy(&wmax, &wb, 4);
+    const float wscale = x2_weight_scale(wmax);
+    hipLaunchKernelGGL(split_planes_f16_kernel, dim3(8192), dim3(256), 0, 0, W, wscale, W2, (size_t)s.N * s.K);
+    const float acc_scale = 1.0f / (wscale * X2_ASCALE);
+
+    // accuracy rows
+    const int nr = 64;
+    std::vector<int> hrows(nr);
+    for (int i = 0; i < nr; ++i) hrows[i] = (int)((i * 1403ll + 17) % s.M);
+    int* drows; double *ref, *mag;
+    hipMalloc(&drows, nr * sizeof(int)); hipMalloc(&ref, sizeof(double) * nr * s.N); hipMalloc(&mag, sizeof(double) * nr * s.N);
+    hipMemcpy(drows, hrows.data(), nr * sizeof(int), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(ref64, dim3((nr * s.N + 255) / 256), dim3(256), 0, 0, A, W, drows, nr, s.N, s.K, ref, mag);
+    std::vector<double> hr(nr * s.N), hm(nr * s.N);
+    hipMemcpy(hr.data(), ref, hr.size() * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(hm.data(), mag, hm.size() * 8, hipMemcpyDeviceToHost);
+
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    for (const auto& path : paths) {
+      GemmEpi e{}; e.out0 = C; e.ld0 = s.N;
+      int grid = 0;
+      auto run = [&](bool stamp) {
+        GemmEpi ee = e;
+        ee.stamps = stamp ? stamps : nullptr;
+        if (path == "f32") {
+          grid = gemm_grid<TileLarge>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_f32_nt_kernel<EPI_BIAS, TileLarge>), dim3(grid), dim3(TileLarge::THREADS), 0, 0,
+                             A, s.K, W, s.K, s.M, s.N, s.K, ee);
+        } else if (path == "x3") {
+          grid = gemm_x3_grid<X3Large>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS, X3Large>), dim3(grid), dim3(X3Large::THREADS), 0, 0,
+                             A, s.K, W3, s.K, (size_t)s.N * s.K, s.M, s.N, s.K, ee);
+        } else {
+          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_x2f16_nt_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+                             A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
+        }
+      };
+      run(false); hipDeviceSynchronize();
+      hipEventRecord(a); run(false); hipEventRecord(b); hipEventSynchronize(b);
+      float ms1; hipEventElapsedTime(&ms1, a, b);
+      const int reps = std::max(2, (int)(1500.f / ms1));
+      for (int i = 0; i < reps; ++i) run(false);
+      hipEventRecord(a);
+      for (int i = 0; i < reps; ++i) run(false);
+      hipEventRecord(b); hipEventSynchronize(b);
+      float ms; hipEventElapsedTime(&ms, a, b);
+      ms /= reps;
+      run(true);  // stamped launch right after the sustained run: clock under load
+      hipDeviceSynchronize();
+      std::vector<unsigned long long> hs(2 * grid);
+      hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost);
+      std::vector<double> clk;
+      for (int g = 0; g < grid; ++g)
+        if (hs[2 * g + 1] > 0) clk.push_back((double)hs[2 * g] / (double)hs[2 * g + 1] * 100.0);  // MHz
+      std::sort(clk.begin(), clk.end());
+      const double mhz = clk.empty() ? 0 : clk[clk.size() / 2];
+      run(false); hipDeviceSynchronize();
+      double emax = 0, erms = 0;
+      std::vector<float> row(s.N);
+      for (int i = 0; i < nr; ++i) {
+        hipMemcpy(row.data(), C + (size_t)hrows[i] * s.N, s.N * 4, hipMemcpyDeviceToHost);
+        for (int n = 0; n < s.N; ++n) {
+          const double err = fabs(row[n] - hr[i * s.N + n]) / hm[i * s.N + n];
+          emax = std::max(emax, err);
+          erms += err * err;
+        }
+      }
+      unsigned hflag = 0;
+      hipMemcpy(&hflag, flag, 4, hipMemcpyDeviceToHost);
+      const double fl = 2.0 * s.M * (double)s.N * s.K;
+      printf("{\"shape\": \"%s\", \"path\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"a_dist\": \"%s\", "
+             "\"ms\": %.3f, \"tflops\": %.1f, \"clock_mhz\": %.0f, \"err_max\": %.3e, \"err_rms\": %.3e, "
+             "\"range_flag\": %u, \"err_unit\": \"|C - C_fp64| / sum_k |a_k w_k|\"}\n",
+             s.name, path.c_str(), s.M, s.N, s.K, s.gelu ? "gelu(3N(0,1))" : "N(0,1)", ms, fl / (ms * 1e-3) / 1e12,
+             mhz, emax, sqrt(erms / ((double)nr * s.N)), hflag);
+      fflush(stdout);
+    }
+    hipFree(A); hipFree(W); hipFree(W3); hipFree(W2); hipFree(C); hipFree(flag); hipFree(wmax_bits);
+    hipFree(stamps); hipFree(drows); hipFree(ref); hipFree(mag);
+  }
+  return 0;
+}
