@@ -211,6 +211,18 @@ int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
                    size_t wps, float w_scale, const float* bias, float* C,
                    int32_t ldc, int32_t M, int32_t N, int32_t K,
                    uint32_t* range_flag, void* stream);
+/* The X2F16 activation format the engine's producers write for every GEMM
+ * input: logical [rows][K] -> halves [rows][2][K] (plane 0 = fp16(16 a),
+ * plane 1 = fp16(16 a - plane 0)); *range_flag (may be NULL) |= 1 if
+ * |a| >= 4095. */
+int tvr_split_rows_f16(const float* a, int32_t lda, uint16_t* out, int32_t rows,
+                       int32_t K, uint32_t* range_flag, void* stream);
+/* The engine's X2F16 GEMM: A in the activation format above (lda logical
+ * elements per row, >= K), W planes as tvr_split_planes_f16 builds them. */
+int tvr_gemm_x2f16_planar(const uint16_t* A, int32_t lda, const uint16_t* W,
+                          int32_t ldw, size_t wps, float w_scale,
+                          const float* bias, float* C, int32_t ldc, int32_t M,
+                          int32_t N, int32_t K, void* stream);
 /* TransformerLens LayerNormPre over rows: (x - mean) / sqrt(var + eps) */
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
                   int32_t rows, int32_t d, float eps, void* stream);

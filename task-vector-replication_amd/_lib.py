@@ -101,6 +101,11 @@ SIGNATURES = {
                                       ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p, ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p]),
+    "tvr_split_rows_f16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "tvr_gemm_x2f16_planar": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                             ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
 }

@@ -206,10 +206,16 @@ hipEvent_t prof_event(tvr_model* m) {
   return e;
 }
 
-int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M, int N,
+// C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] or, with a_split, the
+// X2F16 activation format (split.hpp: lda logical elements per row); split A
+// needs the X2F16 weight planes (W.h) and runs the LDS-DMA planar kernel.
+int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, int ldw, int M, int N,
                 int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr,
                 unsigned* range_flag = nullptr) {
   if (M <= 0 || N <= 0) return TVR_OK;
+  if (a_split && !W.h) return fail(TVR_ERR_INVALID, "gemm: split activations need the X2F16 weight planes");
+  if (epi == EPI_SPLIT_GELU_X2 && !a_split)
+    return fail(TVR_ERR_INVALID, "gemm: the split-GELU epilogue belongs to the X2F16 path");
   if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0))
     return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes; K=" +
                                          std::to_string(K) + ")");
@@ -222,17 +228,24 @@ int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M,
   const bool large = gemm_use_large(M, N);
 #define TVR_GEMM_LAUNCH(E, TL)                                                                  \
   hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
-                     st, A, lda, W.f, ldw, M, N, K, ep)
+                     st, Af, lda, W.f, ldw, M, N, K, ep)
 #define TVR_X3_LAUNCH(E, TL)                                                                      \
   hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
-                     0, st, A, lda, W.x, ldw, W.wps, M, N, K, ep)
+                     0, st, Af, lda, W.x, ldw, W.wps, M, N, K, ep)
   unsigned* flag = m ? m->range_flag : range_flag;
   const float acc_scale = 1.0f / (W.wscale * X2_ASCALE);
+  const float* Af = static_cast<const float*>(A);
+  const uint16_t* Ah = static_cast<const uint16_t*>(A);
+#define TVR_X2P_LAUNCH(E, TL)                                                                            \
+  hipLaunchKernelGGL((gemm_x2f16_planar_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
+                     st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
-                     st, A, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
+                     st, Af, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
 #define TVR_GEMM_PICK(E)                                    \
-  if (W.h) {                                                \
+  if (a_split) {                                            \
+    if (large) TVR_X2P_LAUNCH(E, X2Large); else TVR_X2P_LAUNCH(E, X2Small);       \
+  } else if (W.h) {                                         \
     if (large) TVR_X2_LAUNCH(E, X2Large); else TVR_X2_LAUNCH(E, X2Small);         \
   } else if (W.x) {                                         \
     if (large) TVR_X3_LAUNCH(E, X3Large); else TVR_X3_LAUNCH(E, X3Small);         \
@@ -242,54 +255,71 @@ int launch_gemm(int epi, const float* A, int lda, const MatW& W, int ldw, int M,
   switch (epi) {
     case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
     case EPI_SPLIT_GELU: TVR_GEMM_PICK(EPI_SPLIT_GELU); break;
+    case EPI_SPLIT_GELU_X2:
+      if (large) TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Large); else TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Small);
+      break;
     default: TVR_GEMM_PICK(EPI_RESID); break;
   }
 #undef TVR_GEMM_PICK
 #undef TVR_X3_LAUNCH
 #undef TVR_X2_LAUNCH
+#undef TVR_X2P_LAUNCH
 #undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
     const double wbytes = W.x ? 6.0 : 4.0;  // W read once per launch: fp32, 3 bf16 or 2 fp16 planes
-    m->prof_recs.push_back({ev0, ev1, epi, 2.0 * M * N * (double)K,
+    m->prof_recs.push_back({ev0, ev1, epi == EPI_SPLIT_GELU_X2 ? (int)EPI_SPLIT_GELU : epi, 2.0 * M * N * (double)K,
                             4.0 * ((double)M * K + (double)M * N) + wbytes * N * (double)K});
   }
   return TVR_OK;
 }
 
-int launch_lnpre(const float* x, int ldx, const int32_t* idx, float* y, int ldy, int rows,
-                 int d, float eps, hipStream_t st) {
+// y: fp32 [rows][ldy] or (split) the X2F16 activation format
+int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
+                 int d, float eps, bool split, hipStream_t st) {
   if (rows <= 0) return TVR_OK;
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
     return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
   const int rows_per_block = 4;
-  hipLaunchKernelGGL(lnpre_kernel, dim3((rows + rows_per_block - 1) / rows_per_block),
-                     dim3(64 * rows_per_block), 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+  const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
+  if (split)
+    hipLaunchKernelGGL(lnpre_kernel<true>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+  else
+    hipLaunchKernelGGL(lnpre_kernel<false>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
 
-// Activation buffers of one launch sequence.
+// Activation buffers of one launch sequence.  In X2F16 mode (`split`) xn and
+// a2 hold the split fp16 activation format (split.hpp), same bytes.
 struct Acts {
   float* resid;   // [R][d]
   float* xn;      // [R][d]
   float* qkv;     // [R][3d]
   float* a2;      // [R][K2]  (z | gelu(mlp-in))
+  bool split;
 };
 
+// z: the z columns of a2 (fp32, or split); zf: optional fp32 copy [rows][d]
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
-                     int n_seqs, int maxT, float* z, hipStream_t st) {
+                     int n_seqs, int maxT, void* z, bool split, float* zf, hipStream_t st) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const size_t smem = attention_smem_bytes(maxT, c.d_head);
+  const void* kern = split ? (const void*)attention_kernel<true> : (const void*)attention_kernel<false>;
   if (smem > 64 * 1024)
-    TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)smem));
-  hipLaunchKernelGGL(attention_kernel, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
-                     cache_qkv, 3 * d, d_seqs, z, m->K2, m->rot_cos, m->rot_sin, d, c.d_head, c.rotary_dim,
-                     1.0f / std::sqrt((float)c.d_head));
+    TVR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  const float inv_scale = 1.0f / std::sqrt((float)c.d_head);
+  if (split)
+    hipLaunchKernelGGL(attention_kernel<true>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
+                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,
+                       c.d_head, c.rotary_dim, inv_scale);
+  else
+    hipLaunchKernelGGL(attention_kernel<false>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
+                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,
+                       c.d_head, c.rotary_dim, inv_scale);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
@@ -297,21 +327,37 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
 // One transformer block over the first R rows (Pythia parallel residual):
 //   x = LNPre(resid); [qkv | h] = x @ W1^T + b1; z = attn(qkv); resid += [z|gelu h] @ W2^T + b2
 // (run_block computes up to z; run_block_out the second projection.)
+// The QKV+MLP-in epilogue: Q|K|V fp32 to qkv (row stride 3d), GELU(h) into
+// the a2 columns after z (fp32, or split).
+GemmEpi epi_qkv_mlpin(tvr_model* m, const float* b1, float* qkv, const Acts& a) {
+  const int d = m->cfg.d_model;
+  GemmEpi e{};
+  e.bias = b1;
+  e.out0 = qkv;
+  e.ld0 = 3 * d;
+  e.n_split = 3 * d;
+  if (a.split) {
+    e.out1h = reinterpret_cast<uint16_t*>(a.a2) + d;
+    e.ld1h = 2 * m->K2;
+    e.ps1h = m->K2;
+    e.range_flag = m->range_flag;
+  } else {
+    e.out1 = a.a2 + d;
+    e.ld1 = m->K2;
+  }
+  return e;
+}
+
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
-              Acts& a, float* qkv_out, const float* cache_qkv, hipStream_t st) {
+              Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, st));
-  GemmEpi e1{};
-  e1.bias = w.b1;
-  e1.out0 = qkv_out;
-  e1.ld0 = 3 * d;
-  e1.out1 = a.a2 + d;
-  e1.ld1 = m->K2;
-  e1.n_split = 3 * d;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l], d, R, m->D1, d, e1, st, m));
-  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st);
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.split, st));
+  const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
+  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split, m->w1[l], d, R, m->D1, d,
+                      e1, st, m));
+  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.split, zf, st);
 }
 
 // The last layer when only each sequence's LAST row is read afterwards (patch
@@ -322,28 +368,24 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
 // (nothing downstream reads the final residual).
 int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT, Acts& a,
                         const float* cache_qkv, const int32_t* d_last, int n_last, bool write_out,
-                        hipStream_t st) {
+                        float* zf, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, st));
-  GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.split, st));
+  GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row (all below n_split: no GELU)
   kv.bias = w.b1 + d;
   kv.out0 = a.qkv + d;
   kv.ld0 = 3 * d;
   kv.n_split = 2 * d;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l].rows((size_t)d * d), d, R, 2 * d, d, kv, st, m));
-  GemmEpi e1{};  // all columns for the last rows, gathered and scattered in place
-  e1.bias = w.b1;
-  e1.out0 = a.qkv;
-  e1.ld0 = 3 * d;
-  e1.out1 = a.a2 + d;
-  e1.ld1 = m->K2;
-  e1.n_split = 3 * d;
+  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split,
+                      m->w1[l].rows((size_t)d * d), d, R, 2 * d, d, kv, st, m));
+  GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);  // all columns for the last rows, gathered and scattered in place
   e1.a_rows = d_last;
   e1.out_rows = d_last;
-  TVR_TRY(launch_gemm(EPI_SPLIT_GELU, a.xn, d, m->w1[l], d, n_last, m->D1, d, e1, st, m));
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, st));
+  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split, m->w1[l], d, n_last, m->D1,
+                      d, e1, st, m));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.split, zf, st));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
   e2.bias = w.b2;
@@ -353,7 +395,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e2.ldr = d;
   e2.a_rows = d_last;
   e2.out_rows = d_last;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.split, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
 }
 
 int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
@@ -365,24 +407,24 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
   e2.ld0 = d;
   e2.resid = a.resid;
   e2.ldr = d;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.split, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
 }
 
 // Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
 int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int32_t* d_targets,
               int n, float* xf, float* logits_ws, float* out_prob, int32_t* out_topk, int topk,
-              float* out_logits, hipStream_t st) {
+              float* out_logits, bool split, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model, V = c.d_vocab;
   for (int s = 0; s < n; s += kFinalChunk) {
     const int cn = std::min(kFinalChunk, n - s);
-    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, st));
+    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, split, st));
     float* lg = out_logits ? out_logits + (size_t)s * V : logits_ws;
     GemmEpi e{};
     e.bias = m->b_unembed;
     e.out0 = lg;
     e.ld0 = V;
-    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, m->wu, d, cn, V, d, e, st, m));
+    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, split, m->wu, d, cn, V, d, e, st, m));
     hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
                        d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
                        out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
@@ -715,6 +757,8 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   const size_t o_xf = cv.take<float>((size_t)FC * d);
   const size_t o_lg = out_logits ? 0 : cv.take<float>((size_t)FC * c.d_vocab);
   const size_t o_cap = capture_zsum ? cv.take<float>((size_t)CAP_GROUPS * d) : 0;
+  // fp32 hook_z for the capture when no trace slot receives it
+  const size_t o_zf = (capture_zsum && !trace) ? cv.take<float>((size_t)R * d) : 0;
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -725,8 +769,9 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   ub.add(o_tg, tg);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
+  const bool split = m->gemm_mode == TVR_GEMM_X2F16;
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), trace ? nullptr : (float*)(base + o_qkv),
-         (float*)(base + o_a2)};
+         (float*)(base + o_a2), split};
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const int32_t* d_last = (const int32_t*)(base + o_last);
   const size_t tstride = trace ? (size_t)trace->max_tokens * d : 0;
@@ -743,24 +788,23 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
       TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, (size_t)R * d * sizeof(float),
                              hipMemcpyDeviceToDevice, st));
     float* qkv = trace ? trace->qkv + (size_t)l * 3 * tstride : a.qkv;
+    // attention writes the fp32 hook_z straight into the trace (or the capture buffer)
+    float* zf = trace ? trace->z + l * tstride : (capture_zsum ? (float*)(base + o_zf) : nullptr);
     const bool want_out = out_prob || out_topk || out_logits;
     if (trim && l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, R, (const SeqDesc*)(base + o_seqs_last), n_seq, maxT, a, nullptr,
-                                  d_last, n_seq, want_out, st));
+                                  d_last, n_seq, want_out, zf, st));
     } else {
-      TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, st));
+      TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, zf, st));
     }
     if (capture_zsum) {
       float* part = (float*)(base + o_cap);
       hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
-                         a.a2, m->K2, d_last, n_seq, part, d);
+                         zf, d, d_last, n_seq, part, d);
       hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part,
                          capture_zsum + (size_t)l * d, d);
       TVR_HIP(hipGetLastError());
     }
-    if (trace)
-      TVR_HIP(hipMemcpy2DAsync(trace->z + l * tstride, d * sizeof(float), a.a2, m->K2 * sizeof(float),
-                               d * sizeof(float), R, hipMemcpyDeviceToDevice, st));
     if (!(trim && l == L - 1)) TVR_TRY(run_block_out(m, l, R, a, st));
   }
   if (trace) {
@@ -773,7 +817,8 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   }
   if (out_prob || out_topk || out_logits)
     TVR_TRY(run_final(m, a.resid, d_last, (const int32_t*)(base + o_tg), n_seq, (float*)(base + o_xf),
-                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, st));
+                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, split,
+                      st));
   return TVR_OK;
 }
 
@@ -903,8 +948,9 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   ub.add(o_tg, tg);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
+  const bool split = m->gemm_mode == TVR_GEMM_X2F16;
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), (float*)(base + o_qkv),
-         (float*)(base + o_a2)};
+         (float*)(base + o_a2), split};
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const EntryDesc* d_ents = (const EntryDesc*)(base + o_ents);
   const size_t tstride = (size_t)trace->max_tokens * d;
@@ -933,16 +979,16 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     const float* cache = trace->qkv + (size_t)l * 3 * tstride;
     if (l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), cnt_le[l], maxT, a, cache,
-                                  (const int32_t*)(base + o_last_sorted), cnt_le[l], true, st));
+                                  (const int32_t*)(base + o_last_sorted), cnt_le[l], true, nullptr, st));
     } else {
-      TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv, cache, st));
+      TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv, cache, nullptr, st));
       TVR_TRY(run_block_out(m, l, Rl, a, st));
     }
   }
   TVR_TRY(enter(L));
   return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
                    (float*)(base + o_xf), out_logits ? nullptr : (float*)(base + o_lg), out_prob,
-                   out_topk, topk, out_logits, st);
+                   out_topk, topk, out_logits, split, st);
 }
 
 int tvr_project_heads(tvr_model* m, const float* zsum, float* out, void* stream) {
@@ -962,7 +1008,7 @@ int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw, const
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, MatW{W}, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, false, MatW{W}, ldw, M, N, K, e, (hipStream_t)stream);
 }
 
 int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream) {
@@ -981,7 +1027,8 @@ int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, W, nullptr, wps, 1.0f}, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, false, MatW{nullptr, W, nullptr, wps, 1.0f}, ldw, M, N, K, e,
+                     (hipStream_t)stream);
 }
 
 int tvr_split_planes_f16(const float* w, float scale, uint16_t* out, size_t n, void* stream) {
@@ -1002,14 +1049,39 @@ int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw, 
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
+  return launch_gemm(EPI_BIAS, A, lda, false, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
                      (hipStream_t)stream, nullptr, range_flag);
+}
+
+int tvr_split_rows_f16(const float* a, int32_t lda, uint16_t* out, int32_t rows, int32_t K, uint32_t* range_flag,
+                       void* stream) {
+  if (!a || !out || rows < 0 || K <= 0 || lda < K) return fail(TVR_ERR_INVALID, "tvr_split_rows_f16: bad argument");
+  const size_t n = (size_t)rows * K;
+  if (n == 0) return TVR_OK;
+  hipLaunchKernelGGL(split_rows_f16_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, a, lda, out, rows, K, range_flag);
+  TVR_HIP(hipGetLastError());
+  return TVR_OK;
+}
+
+int tvr_gemm_x2f16_planar(const uint16_t* A, int32_t lda, const uint16_t* W, int32_t ldw, size_t wps,
+                          float w_scale, const float* bias, float* C, int32_t ldc, int32_t M, int32_t N, int32_t K,
+                          void* stream) {
+  if (!A || !W || !C || M < 0 || N < 0 || K <= 0 || lda < K || !(w_scale > 0.0f) ||
+      wps < (size_t)ldw * (N > 0 ? N - 1 : 0) + K)
+    return fail(TVR_ERR_INVALID, "tvr_gemm_x2f16_planar: bad argument");
+  GemmEpi e{};
+  e.bias = bias;
+  e.out0 = C;
+  e.ld0 = ldc;
+  return launch_gemm(EPI_BIAS, A, lda, true, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
+                     (hipStream_t)stream);
 }
 
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy, int32_t rows, int32_t d, float eps,
                   void* stream) {
   if (!x || !y || rows < 0 || d <= 0) return fail(TVR_ERR_INVALID, "tvr_lnpre_f32: bad argument");
-  return launch_lnpre(x, ldx, nullptr, y, ldy, rows, d, eps, (hipStream_t)stream);
+  return launch_lnpre(x, ldx, nullptr, y, ldy, rows, d, eps, false, (hipStream_t)stream);
 }
 
 }  // extern "C"

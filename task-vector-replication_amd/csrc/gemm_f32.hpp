@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "split.hpp"
+
 namespace tvr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -44,6 +46,7 @@ enum GemmEpiKind {
   EPI_BIAS = 0,        // out0 = acc + bias
   EPI_SPLIT_GELU = 1,  // col < n_split: out0 = acc + bias ; else out1 = gelu(acc + bias)
   EPI_RESID = 2,       // out0 = acc + bias + resid   (in place allowed: out0 == resid)
+  EPI_SPLIT_GELU_X2 = 3,  // EPI_SPLIT_GELU with the GELU columns stored as fp16 split planes (split.hpp)
 };
 
 struct GemmEpi {
@@ -59,6 +62,12 @@ struct GemmEpi {
   // a_rows[m], output row m (and its residual) lives at out_rows[m].
   const int32_t* a_rows;
   const int32_t* out_rows;
+  // EPI_SPLIT_GELU_X2: GELU column c of row r goes to out1h + r*ld1h + c
+  // (plane 0) and + ps1h (plane 1), both in halves; range_flag as split.hpp.
+  uint16_t* out1h;
+  int ld1h;
+  int ps1h;
+  unsigned* range_flag;
   // Diagnostics only (tools/gemm_probe.hip; the engine passes nullptr): per
   // block {Δs_memtime, Δs_memrealtime} to read the shader clock under load.
   unsigned long long* stamps;
@@ -67,6 +76,26 @@ struct GemmEpi {
 __device__ __forceinline__ float gelu_erf(float x) {
   // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu"
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+// One output element of the fused epilogues (v = acc + bias already).
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemmEpi& ep, size_t orow, int col, float v) {
+  if constexpr (EPI == EPI_BIAS) {
+    ep.out0[orow * ep.ld0 + col] = v;
+  } else if constexpr (EPI == EPI_SPLIT_GELU) {
+    if (col < ep.n_split)
+      ep.out0[orow * ep.ld0 + col] = v;
+    else
+      ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
+  } else if constexpr (EPI == EPI_SPLIT_GELU_X2) {
+    if (col < ep.n_split)
+      ep.out0[orow * ep.ld0 + col] = v;
+    else
+      store_split(ep.out1h + orow * ep.ld1h + (col - ep.n_split), ep.ps1h, gelu_erf(v), ep.range_flag);
+  } else {
+    ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
+  }
 }
 
 // Shared epilogue of every GEMM kernel: wave tile of TM x TN 32x32
@@ -87,17 +116,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmEpi& ep, const f32x16 (&
         const int row = row_base + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= M) continue;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
-        const float v = acc[i][j][r] + bcol;
-        if constexpr (EPI == EPI_BIAS) {
-          ep.out0[orow * ep.ld0 + col] = v;
-        } else if constexpr (EPI == EPI_SPLIT_GELU) {
-          if (col < ep.n_split)
-            ep.out0[orow * ep.ld0 + col] = v;
-          else
-            ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
-        } else {
-          ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
-        }
+        epi_store<EPI>(ep, orow, col, acc[i][j][r] + bcol);
       }
     }
   }

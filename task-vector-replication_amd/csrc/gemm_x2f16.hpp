@@ -39,15 +39,13 @@
 #include <cmath>
 
 #include "gemm_f32.hpp"
+#include "split.hpp"
 
 namespace tvr {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
-constexpr float X2_ASCALE = 16.0f;
-constexpr float X2_FP16_OVERFLOW = 65520.0f;  // fp16(x) is inf from here (round to nearest)
 
 template <int BM_, int BN_, int WM_, int WN_>
 struct X2TileT {
@@ -63,6 +61,13 @@ struct X2TileT {
 };
 using X2Large = X2TileT<256, 256, 2, 4>;  // 8 waves of 128x64, 128 KB LDS
 using X2Small = X2TileT<128, 128, 2, 2>;  // 4 waves of 64x64, 64 KB LDS
+
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land
+// at lds_base + 16 l.  (A non-template wrapper: referenced directly from a
+// kernel template, the builtin suppresses the host-side launch stub.)
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, lds_base, 16, 0, 0);
+}
 
 // fp16 offset of (row, 16-B chunk) in a swizzled [rows][32] plane
 __device__ __forceinline__ int x2_swz(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 2) & 3)) << 3); }
@@ -244,6 +249,159 @@ inline float x2_weight_scale(float wmax) {
   int e = 0;
   (void)std::frexp(wmax, &e);  // wmax = f * 2^e, f in [0.5, 1)
   return std::ldexp(1.0f, 15 - e);
+}
+
+// Epilogue for 16x16 accumulators (v_mfma_f32_16x16x32_*: col = lane&15,
+// row = 4*(lane>>4) + r).
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue16(const GemmEpi& ep, const f32x4 (&acc)[TM][TN], int M, int N,
+                                                int row_base, int col_base, int lane) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + j * 16 + (lane & 15);
+    if (col >= N) continue;
+    const float bcol = ep.bias ? ep.bias[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row_base + i * 16 + 4 * (lane >> 4) + r;
+        if (row >= M) continue;
+        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
+        epi_store<EPI>(ep, orow, col, acc[i][j][r] + bcol);
+      }
+    }
+  }
+}
+
+// fp16 offset of (row, 16-B chunk) for the 16x16x32 operand reads (lane l:
+// row l&15, chunk l>>4): chunk ^= 2 * bit 3 of the row is conflict-free for
+// all four ds_read_b128 lane groups.
+__device__ __forceinline__ int x2_swz16(int row, int chunk) { return row * 32 + ((chunk ^ (((row >> 3) & 1) << 1)) << 3); }
+
+// ---------------------------------------------------------------------------
+// The engine's X2F16 kernel.  A arrives as two fp16 planes already (its
+// producer wrote them: split.hpp; A plane p at A + p * aps, row stride lda
+// halves), so staging is a pure copy and both operands go global -> LDS by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write): per K step each
+// wave issues 8 x 1 KB pieces (16 rows x 64 B of one plane), 64 per 256-row
+// block.  The XOR swizzle of x2_swz16 moves to the per-lane source address
+// (a piece's LDS image is lane-linear).  Tile k+1's pieces fly while tile k's
+// MFMAs run; one barrier per K step (its vmcnt(0) retires them).
+// MFMA shape v_mfma_f32_16x16x32_f16: the chip holds a higher clock on it
+// than on 32x32x16 (MI355X_MICROARCH.md, DVFS item 7); measured 398-427 TF
+// fp32-equivalent against 367-377 for the same kernel on 32x32x16 and
+// 342-345 for gemm_x2f16_nt_kernel (profiles/gemm_split_probe_r01.jsonl).
+template <int EPI, class TL>
+__global__ void __launch_bounds__(TL::THREADS, 2)
+gemm_x2f16_planar_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
+                     size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
+  constexpr int BM = TL::BM, BN = TL::BN, NT = TL::THREADS;
+  constexpr int BK = TL::BK, PL = TL::PLANE;
+  constexpr int TM = BM / TL::WM / 16, TN = BN / TL::WN / 16;
+  constexpr int PIECES = 2 * 2 * BM / 16;
+  constexpr int PER_WAVE = PIECES / (NT / 64);
+  static_assert(PER_WAVE * (NT / 64) == PIECES && (BM / 16) % PER_WAVE == 0, "piece map");
+  const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 4 * PL];
+  auto sA = [&](int b, int p) { return lds + (size_t)(b * 4 + p) * PL; };
+  auto sB = [&](int b, int p) { return lds + (size_t)(b * 4 + 2 + p) * PL; };
+
+  const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GEMM_GROUP_M * nbn;
+  const int grp = wg / per_group;
+  const int first_m = grp * GEMM_GROUP_M;
+  const int gsz = min(nbm - first_m, GEMM_GROUP_M);
+  const int in_grp = wg - grp * per_group;
+  const int m0 = (first_m + in_grp % gsz) * BM, n0 = (in_grp / gsz) * BN;
+
+  const int t = threadIdx.x;
+  const int wave = t >> 6, lane = t & 63;
+  const int first = wave * PER_WAVE;
+  const int slot = first / (BM / 16);
+  const int prow0 = (first % (BM / 16)) * 16;
+  const bool is_w = slot >= 2;
+  const int plane = slot & 1;
+  const int lrow = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lrow >> 3) & 1) << 1);  // x2_swz16 of row 16i + lrow
+  const uint16_t* src[PER_WAVE];
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int row = prow0 + 16 * i + lrow;
+    if (is_w) {
+      src[i] = W + plane * wps + (size_t)min(n0 + row, N - 1) * ldw + lchunk * 8;
+    } else {
+      const int am = min(m0 + row, M - 1);
+      src[i] = A + plane * aps + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + lchunk * 8;
+    }
+  }
+  const int dst0 = slot * PL + prow0 * 32;
+  auto issue = [&](int k0, int b) {
+    _Float16* d = lds + (size_t)b * 4 * PL + dst0;
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + k0, d + i * 16 * 32);
+  };
+
+  const int wr = wave / TL::WN, wc = wave % TL::WN;
+  const int aoff = x2_swz16(wr * (BM / TL::WM) + (lane & 15), lane >> 4);
+  const int boff = x2_swz16(wc * (BN / TL::WN) + (lane & 15), lane >> 4);
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{};
+  auto compute = [&](int b) {
+    f16x8 fb[2][TN];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[p][j] = *(const f16x8*)(sB(b, p) + boff + j * 16 * 32);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const f16x8 a0 = *(const f16x8*)(sA(b, 0) + aoff + i * 16 * 32);
+      const f16x8 a1 = *(const f16x8*)(sA(b, 1) + aoff + i * 16 * 32);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, fb[0][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb[1][j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb[0][j], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+    }
+  };
+
+  const int nk = K / BK;
+  issue(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue((kt + 1) * BK, (kt + 1) & 1);
+    compute(kt & 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= acc_scale;
+  gemm_epilogue16<EPI, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lane);
+  if (ep.stamps && t == 0) {
+    ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
+    ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+  }
+}
+
+// A [M][K] fp32 -> 2 fp16 planes [2][M][K] of a * X2_ASCALE (probe / tests)
+__global__ void split_act_f16_kernel(const float* __restrict__ a, uint16_t* __restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float x = a[i] * X2_ASCALE;
+    const _Float16 h0 = (_Float16)x;
+    out[i] = __builtin_bit_cast(uint16_t, h0);
+    out[n + i] = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)h0));
+  }
 }
 
 template <class TL>

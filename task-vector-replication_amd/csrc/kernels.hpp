@@ -10,6 +10,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "split.hpp"
+
 namespace tvr {
 
 // ---------------------------------------------------------------------------
@@ -70,17 +72,19 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
 
 // ---------------------------------------------------------------------------
 // LayerNormPre (TL, after fold_ln): x -= mean(x); x /= sqrt(mean(x^2) + eps).
-// One wave per row; rows optionally gathered through `row_idx`.
+// One wave per row; rows optionally gathered through `row_idx`.  SPLIT: y is
+// the X2F16 activation format (split.hpp; ldy counts logical elements); the
+// outputs are bounded by sqrt(d), so no range check.
+template <bool SPLIT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
-                             float* __restrict__ y, int ldy, int rows, int d,
+                             void* __restrict__ y, int ldy, int rows, int d,
                              float eps) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;
   const int src = row_idx ? row_idx[r] : r;
   const float4* xr = (const float4*)(x + (size_t)src * ldx);
-  float4* yr = (float4*)(y + (size_t)r * ldy);
   const int d4 = d >> 2;
   float s = 0.f;
   for (int c = lane; c < d4; c += 64) {
@@ -99,7 +103,14 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     float4 v = xr[c];
     v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;
     v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
-    yr[c] = v;
+    if constexpr (SPLIT) {
+      uint16_t* yr = (uint16_t*)y + (size_t)r * 2 * ldy + 4 * c;
+      const SplitF16 a = split_f16(v.x), b = split_f16(v.y), e = split_f16(v.z), f = split_f16(v.w);
+      *(uint2*)yr = make_uint2(a.h0 | ((unsigned)b.h0 << 16), e.h0 | ((unsigned)f.h0 << 16));
+      *(uint2*)(yr + ldy) = make_uint2(a.h1 | ((unsigned)b.h1 << 16), e.h1 | ((unsigned)f.h1 << 16));
+    } else {
+      ((float4*)((float*)y + (size_t)r * ldy))[c] = v;
+    }
   }
 }
 
@@ -112,7 +123,9 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
 // barrier no block-level barrier remains.  One score per lane per 64 keys,
 // wave-shuffle softmax, one output dim per lane.
 //   qkv  [rows][3d]: q at h*dh, k at d + h*dh, v at 2d + h*dh (pre-rotary)
-//   z    [rows][ldz]: written at h*dh  (attn.hook_z)
+//   z    [rows][ldz]: written at h*dh  (attn.hook_z), the next GEMM's input:
+//        fp32, or SPLIT: the X2F16 format (split.hpp), range-checked into flag
+//   zf   [rows][ldzf] fp32 copy (trace / capture) or nullptr
 constexpr int ATT_THREADS = 256;
 constexpr int ATT_MAX_T = 128;
 
@@ -124,10 +137,12 @@ inline size_t attention_smem_bytes(int T, int dh) {
   return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
 }
 
+template <bool SPLIT>
 __global__ void __launch_bounds__(ATT_THREADS)
 attention_kernel(const float* __restrict__ qkv, int ldq,
                  const float* __restrict__ cache, int ldc,
-                 const SeqDesc* __restrict__ seqs, float* __restrict__ z, int ldz,
+                 const SeqDesc* __restrict__ seqs, void* __restrict__ z, int ldz,
+                 float* __restrict__ zf, int ldzf, unsigned* __restrict__ flag,
                  const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                  int d, int dh, int rd, float inv_attn_scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -207,11 +222,15 @@ attention_kernel(const float* __restrict__ qkv, int ldq,
       if (j <= pos) Ps[j] = sc[u] / sum;
     }
     wave_lds_fence();
-    float* zr = z + (size_t)(sd.row0 + i) * ldz + h * dh;
+    const size_t zrow = (size_t)(sd.row0 + i);
     for (int k = lane; k < dh; k += 64) {
       float a = 0.f;
       for (int j = 0; j <= pos; ++j) a += Ps[j] * Vs[j * dhp + k];
-      zr[k] = a;
+      if constexpr (SPLIT)
+        store_split((uint16_t*)z + zrow * 2 * ldz + h * dh + k, ldz, a, flag);
+      else
+        ((float*)z)[zrow * ldz + h * dh + k] = a;
+      if (zf) zf[zrow * ldzf + h * dh + k] = a;
     }
     wave_lds_fence();
   }

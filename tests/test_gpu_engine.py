@@ -109,6 +109,42 @@ def test_gemm_x2f16_matches_torch(M, N, K):
     assert flag.item() == 0
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 1, 32), (37, 130, 64), (300, 257, 320), (1000, 2560, 2560),
+                                   (129, 50304, 64), (4096, 8192, 256), (3001, 17920, 96), (600, 2560, 12800)])
+def test_gemm_x2f16_planar_matches_torch(M, N, K):
+    """The engine's X2F16 GEMM (pre-split activations, LDS-DMA staging,
+    16x16x32 MFMA) meets the fp32 MFMA GEMM's bound."""
+    g = torch.Generator(device="cpu").manual_seed(M * 11 + N)
+    A = torch.randn(M, K, generator=g)
+    A[:, ::5] *= 1e-4
+    W = torch.randn(N, K, generator=g) * 2e-2
+    b = torch.randn(N, generator=g)
+    lib = tvr_amd._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    scale = float(2.0 ** (15 - int(np.frexp(W.abs().max().item())[1])))
+    planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_split_planes_f16(Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
+    lda = K + 32  # a padded logical row: the format's stride is independent of K
+    Ap = torch.zeros(M, lda, device="cuda")
+    Ap[:, :K] = Ad
+    Ah = torch.empty(M, 2, lda, dtype=torch.int16, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    tvr_amd._lib.check(lib.tvr_split_rows_f16(Ap.data_ptr(), lda, Ah.data_ptr(), M, lda, flag.data_ptr(), st),
+                       "split rows")
+    # plane 0 + plane 1 = 16 a within 2^-22 relative (+ half the fp16 subnormal spacing)
+    hs = Ah.view(torch.float16).double().sum(1)[:, :K]
+    assert ((hs - 16 * Ad.double()).abs() <= 2.0 ** -22 * 16 * Ad.double().abs() + 2.0 ** -25).all()
+    C = torch.empty(M, N, device="cuda")
+    tvr_amd._lib.check(lib.tvr_gemm_x2f16_planar(Ah.data_ptr(), lda, planes.data_ptr(), K, N * K, scale,
+                                                 bd.data_ptr(), C.data_ptr(), N, M, N, K, st), "gemm_x2p")
+    ref = A.double() @ W.double().T + b.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    bound = 4e-7 * (A.double().abs() @ W.double().abs().T).max().item() + 1e-6
+    assert err <= bound, (err, bound)
+    assert flag.item() == 0
+
+
 def test_gemm_x2f16_range_flag():
     """An input at the split's range limit (|a| >= 4095) is reported, not hidden."""
     M, N, K = 64, 64, 64
@@ -124,6 +160,11 @@ def test_gemm_x2f16_range_flag():
         flag = torch.zeros(1, dtype=torch.int32, device="cuda")
         tvr_amd._lib.check(lib.tvr_gemm_x2f16(A.data_ptr(), K, planes.data_ptr(), K, N * K, 2.0 ** 16, None,
                                               C.data_ptr(), N, M, N, K, flag.data_ptr(), st), "gemm_x2")
+        assert flag.item() == want, big
+        # the activation-format producers raise the same flag
+        flag.zero_()
+        Ah = torch.empty(M, 2, K, dtype=torch.int16, device="cuda")
+        tvr_amd._lib.check(lib.tvr_split_rows_f16(A.data_ptr(), K, Ah.data_ptr(), M, K, flag.data_ptr(), st), "rows")
         assert flag.item() == want, big
 
 
@@ -388,3 +429,19 @@ def test_batched_fv_helpers_match_reference_loops(tiny_model, tiny_oracle, mean_
                     v = R.assemble_task_vector(ref_mean * 4, cie_ref, i, j + 1)
                     want[i, j] = R.check_accuracy_of_added_task_vector(v, i, ctx, 5, tiny_oracle)
         assert torch.equal(grid, want)
+
+
+def test_x2f16_range_error_is_loud(tiny_cfg, tokenizer):
+    """An activation outside the fp16 split's range fails the call (EngineError)
+    instead of returning inaccurate results; the other modes run the same model."""
+    sd = tvr_amd.weights.synth_hf_state_dict(tiny_cfg, seed=0, std=0.15)
+    for k in list(sd):
+        if k.endswith("mlp.dense_h_to_4h.weight"):
+            sd[k] = sd[k] * 1e5  # GELU(h) ~ 1e5 >> 4095
+    prompts = [[0, 5, 9, 13], [0, 7]]
+    m = tvr_amd.Model.from_hf_state_dict(tiny_cfg, sd, device="cuda", tokenizer=tokenizer, gemm="x2f16")
+    with pytest.raises(tvr_amd._lib.EngineError, match="X2F16"):
+        m.forward_clean(prompts, targets=[1, 2])
+    m.set_gemm("x3bf16")
+    out = m.forward_clean(prompts, targets=[1, 2])
+    assert torch.isfinite(out["prob"]).all()

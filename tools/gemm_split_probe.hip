@@ -2,7 +2,7 @@
 // paths (fp32 MFMA, 3-plane bf16 split, 2-plane fp16 split) at the engine's
 // real shapes, each checked against an fp64 reference on sampled rows.
 //   hipcc --offload-arch=gfx950 -O3 -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
-//   tools/gemm_split_probe [f32|x3|x2 ...]      (default: all three)
+//   tools/gemm_split_probe [f32|x3|x2|x2p ...]   (default: all; x2p = x2 with A pre-split)
 // A is drawn N(0,1) (a LayerNorm output) or GELU(3 N(0,1)) (the MLP-out input:
 // many tiny values, which exercises the fp16 residual plane's range).
 #include <hip/hip_runtime.h>
@@ -44,12 +44,12 @@ __global__ void ref64(const float* A, const float* W, const int* rows, int nr, i
 int main(int argc, char** argv) {
   std::vector<std::string> paths;
   for (int i = 1; i < argc; ++i) paths.push_back(argv[i]);
-  if (paths.empty()) paths = {"f32", "x3", "x2"};
+  if (paths.empty()) paths = {"f32", "x3", "x2", "x2p"};
   struct Shape { const char* name; int M, N, K; int gelu; };
   std::vector<Shape> shapes = {{"qkv_mlpin", 90000, 17920, 2560, 0}, {"o_mlpout", 90000, 2560, 12800, 1}};
   for (auto& s : shapes) {
     float *A, *W, *C;
-    uint16_t *W3, *W2;
+    uint16_t *W3, *W2, *A2;
     unsigned *flag, *wmax_bits;
     unsigned long long* stamps;
     const int maxgrid = gemm_grid<TileSmall>(s.M, s.N);
@@ -57,6 +57,7 @@ int main(int argc, char** argv) {
     hipMalloc(&W, sizeof(float) * (size_t)s.N * s.K);
     hipMalloc(&W3, sizeof(uint16_t) * 3 * (size_t)s.N * s.K);
     hipMalloc(&W2, sizeof(uint16_t) * 2 * (size_t)s.N * s.K);
+    hipMalloc(&A2, sizeof(uint16_t) * 2 * (size_t)s.M * s.K);
     hipMalloc(&C, sizeof(float) * (size_t)s.M * s.N);
     hipMalloc(&flag, 8);
     hipMalloc(&wmax_bits, 8);
@@ -74,6 +75,7 @@ int main(int argc, char** argv) {
     const float wscale = x2_weight_scale(wmax);
     hipLaunchKernelGGL(split_planes_f16_kernel, dim3(8192), dim3(256), 0, 0, W, wscale, W2, (size_t)s.N * s.K);
     const float acc_scale = 1.0f / (wscale * X2_ASCALE);
+    hipLaunchKernelGGL(split_act_f16_kernel, dim3(8192), dim3(256), 0, 0, A, A2, (size_t)s.M * s.K);
 
     // accuracy rows
     const int nr = 64;
@@ -103,6 +105,10 @@ int main(int argc, char** argv) {
           grid = gemm_x3_grid<X3Large>(s.M, s.N);
           hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS, X3Large>), dim3(grid), dim3(X3Large::THREADS), 0, 0,
                              A, s.K, W3, s.K, (size_t)s.N * s.K, s.M, s.N, s.K, ee);
+        } else if (path == "x2p") {
+          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else {
           grid = gemm_x2_grid<X2Large>(s.M, s.N);
           hipLaunchKernelGGL((gemm_x2f16_nt_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
@@ -149,7 +155,7 @@ int main(int argc, char** argv) {
              mhz, emax, sqrt(erms / ((double)nr * s.N)), hflag);
       fflush(stdout);
     }
-    hipFree(A); hipFree(W); hipFree(W3); hipFree(W2); hipFree(C); hipFree(flag); hipFree(wmax_bits);
+    hipFree(A); hipFree(A2); hipFree(W); hipFree(W3); hipFree(W2); hipFree(C); hipFree(flag); hipFree(wmax_bits);
     hipFree(stamps); hipFree(drows); hipFree(ref); hipFree(mag);
   }
   return 0;
