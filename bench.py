@@ -79,18 +79,19 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(family, workload):
-    """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary of
-    this bench command on the same GEMM family (profiles/pmc_gemm_<family>.json,
-    written by tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE
-    passes with the gfx950 x2 FETCH_SIZE correction).  None if absent."""
+def pmc_summary(family, workload):
+    """The committed rocprofv3 PMC summary of this bench command on the same
+    GEMM family (profiles/pmc_gemm_<family>.json, written by
+    tools/prof_summary.py): HBM bytes per GEMM launch from separate FETCH_SIZE /
+    WRITE_SIZE passes (gfx950 x2 FETCH_SIZE correction) and MFMA utilisation
+    from SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE.  (None, None) if absent."""
     p = ROOT / "profiles" / f"pmc_gemm_{family}.json"
     if not p.exists():
         return None, None
     d = json.loads(p.read_text())
     if d.get("family") != family or d.get("workload") != workload:
         return None, None  # counters of another kernel or workload do not apply
-    return d.get("hbm_bytes_per_launch"), f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
+    return d, f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
 
 
 def log(*a):
@@ -207,7 +208,8 @@ def main():
     T = len(prompts[0])
     workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
                 f"{args.kshot}-shot, T={T}")
-    traffic, traffic_src = pmc_traffic(args.gemm, workload)
+    pmc, traffic_src = pmc_summary(args.gemm, workload)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     peak = PEAKS[args.gemm]
     L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
@@ -252,6 +254,7 @@ def main():
                            f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "mfma_util_rocprof": (pmc.get("mfma") or {}).get("all") if pmc else None,
             "algorithmic_bytes_per_launch": round(fam["bytes"] / max(fam["launches"], 1)),
             "launches_per_step": fam["launches"] // args.steps,
             "avg_launch_gflop": round(fam["flops"] / max(fam["launches"], 1) / 1e9, 3),

@@ -236,15 +236,18 @@ int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, in
   const float acc_scale = 1.0f / (W.wscale * X2_ASCALE);
   const float* Af = static_cast<const float*>(A);
   const uint16_t* Ah = static_cast<const uint16_t*>(A);
-#define TVR_X2P_LAUNCH(E, TL)                                                                            \
-  hipLaunchKernelGGL((gemm_x2f16_planar_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
+  const bool vec = x2_epilogue_vec(epi, ep, N);
+#define TVR_X2P_LAUNCH1(E, TL, V)                                                                            \
+  hipLaunchKernelGGL((gemm_x2f16_planar_kernel<E, TL, V>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_X2P_LAUNCH(E, TL) \
+  if (vec) TVR_X2P_LAUNCH1(E, TL, true); else TVR_X2P_LAUNCH1(E, TL, false)
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Af, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
 #define TVR_GEMM_PICK(E)                                    \
   if (a_split) {                                            \
-    if (large) TVR_X2P_LAUNCH(E, X2Large); else TVR_X2P_LAUNCH(E, X2Small);       \
+    if (large) { TVR_X2P_LAUNCH(E, X2Large); } else { TVR_X2P_LAUNCH(E, X2Small); }     \
   } else if (W.h) {                                         \
     if (large) TVR_X2_LAUNCH(E, X2Large); else TVR_X2_LAUNCH(E, X2Small);         \
   } else if (W.x) {                                         \
@@ -256,7 +259,7 @@ int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, in
     case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
     case EPI_SPLIT_GELU: TVR_GEMM_PICK(EPI_SPLIT_GELU); break;
     case EPI_SPLIT_GELU_X2:
-      if (large) TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Large); else TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Small);
+      if (large) { TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Large); } else { TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Small); }
       break;
     default: TVR_GEMM_PICK(EPI_RESID); break;
   }
@@ -264,6 +267,7 @@ int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, in
 #undef TVR_X3_LAUNCH
 #undef TVR_X2_LAUNCH
 #undef TVR_X2P_LAUNCH
+#undef TVR_X2P_LAUNCH1
 #undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {

@@ -47,9 +47,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int MINW_ = 2>
 struct X2TileT {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = 32;
+  static constexpr int MINW = MINW_;  // waves per SIMD the register budget must allow
   static constexpr int THREADS = WM * WN * 64;
   static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static constexpr int LOADS_A = BM * BK / 4 / THREADS;  // float4 of A per thread per K step
@@ -61,6 +62,7 @@ struct X2TileT {
 };
 using X2Large = X2TileT<256, 256, 2, 4>;  // 8 waves of 128x64, 128 KB LDS
 using X2Small = X2TileT<128, 128, 2, 2>;  // 4 waves of 64x64, 64 KB LDS
+using X2Wide = X2TileT<256, 256, 2, 2, 1>;  // 4 waves of 128x128, one per SIMD (512-VGPR budget), 128 KB LDS
 
 // One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land
 // at lds_base + 16 l.  (A non-template wrapper: referenced directly from a
@@ -251,27 +253,80 @@ inline float x2_weight_scale(float wmax) {
   return std::ldexp(1.0f, 15 - e);
 }
 
-// Epilogue for 16x16 accumulators (v_mfma_f32_16x16x32_*: col = lane&15,
-// row = 4*(lane>>4) + r).
-template <int EPI, int TM, int TN>
-__device__ __forceinline__ void gemm_epilogue16(const GemmEpi& ep, const f32x4 (&acc)[TM][TN], int M, int N,
-                                                int row_base, int col_base, int lane) {
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = col_base + j * 16 + (lane & 15);
-    if (col >= N) continue;
-    const float bcol = ep.bias ? ep.bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
+// Epilogue for transposed 16x16 accumulators: the MFMA computes D = W A^T, so
+// lane l holds C[m = 16-row slice + (l & 15)][n = 16-col slice + 4 (l >> 4) + r]
+// for r = 0..3 — four consecutive output columns of one row, stored as one
+// 16-B (fp32) or two 8-B (split planes) vector stores instead of four scalar
+// ones (the 32x32 layouts put rows, not columns, in a lane's registers).
+template <int EPI>
+__device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n0, f32x4 v) {
+  if constexpr (EPI == EPI_BIAS) {
+    *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v;
+  } else if constexpr (EPI == EPI_SPLIT_GELU || EPI == EPI_SPLIT_GELU_X2) {
+    if (n0 < ep.n_split) {  // n_split % 4 == 0: a group never straddles it
+      *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v;
+    } else if constexpr (EPI == EPI_SPLIT_GELU) {
+      const f32x4 g = {gelu_erf(v[0]), gelu_erf(v[1]), gelu_erf(v[2]), gelu_erf(v[3])};
+      *(f32x4*)(ep.out1 + orow * ep.ld1 + (n0 - ep.n_split)) = g;
+    } else {
+      SplitF16 h[4];
+      float amax = 0.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = row_base + i * 16 + 4 * (lane >> 4) + r;
-        if (row >= M) continue;
-        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[row] : (size_t)row;
-        epi_store<EPI>(ep, orow, col, acc[i][j][r] + bcol);
+        const float g = gelu_erf(v[r]);
+        amax = fmaxf(amax, fabsf(g));
+        h[r] = split_f16(g);
+      }
+      uint16_t* p = ep.out1h + orow * ep.ld1h + (n0 - ep.n_split);
+      *(uint2*)p = make_uint2(h[0].h0 | ((unsigned)h[1].h0 << 16), h[2].h0 | ((unsigned)h[3].h0 << 16));
+      *(uint2*)(p + ep.ps1h) = make_uint2(h[0].h1 | ((unsigned)h[1].h1 << 16), h[2].h1 | ((unsigned)h[3].h1 << 16));
+      if (amax * X2_ASCALE >= X2_FP16_OVERFLOW && ep.range_flag) atomicOr(ep.range_flag, 1u);
+    }
+  } else {
+    const f32x4 rr = *(const f32x4*)(ep.resid + orow * ep.ldr + n0);
+    *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v + rr;
+  }
+}
+
+// VEC (chosen on the host by x2_epilogue_vec): N, the row strides and n_split
+// are multiples of 4, so a 4-column group is either wholly in range or out.
+// Without it, element-wise stores (one path per instantiation: both in one
+// body exceed the unroller's budget and the accumulators go to scratch).
+template <int EPI, bool VEC, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue16t(const GemmEpi& ep, const f32x4 (&acc)[TM][TN], int M, int N,
+                                                 int row_base, int col_base, int lane) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n0 = col_base + j * 16 + 4 * (lane >> 4);
+    if (n0 >= N) continue;
+    f32x4 b4 = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b4[r] = n0 + r < N ? ep.bias[n0 + r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = row_base + i * 16 + (lane & 15);
+      if (m >= M) continue;
+      const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
+      const f32x4 v = acc[i][j] + b4;
+      if constexpr (VEC) {
+        epi_store4<EPI>(ep, orow, n0, v);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n0 + r < N) epi_store<EPI>(ep, orow, n0 + r, v[r]);
       }
     }
   }
+}
+
+inline bool x2_epilogue_vec(int EPI, const GemmEpi& ep, int N) {
+  int m = N | ep.ld0;
+  if (EPI == EPI_RESID) m |= ep.ldr;
+  if (EPI == EPI_SPLIT_GELU) m |= ep.ld1 | ep.n_split;
+  if (EPI == EPI_SPLIT_GELU_X2) m |= ep.ld1h | ep.ps1h | ep.n_split;
+  return (m & 3) == 0;
 }
 
 // fp16 offset of (row, 16-B chunk) for the 16x16x32 operand reads (lane l:
@@ -292,8 +347,8 @@ __device__ __forceinline__ int x2_swz16(int row, int chunk) { return row * 32 + 
 // than on 32x32x16 (MI355X_MICROARCH.md, DVFS item 7); measured 398-427 TF
 // fp32-equivalent against 367-377 for the same kernel on 32x32x16 and
 // 342-345 for gemm_x2f16_nt_kernel (profiles/gemm_split_probe_r01.jsonl).
-template <int EPI, class TL>
-__global__ void __launch_bounds__(TL::THREADS, 2)
+template <int EPI, class TL, bool VEC = true, int PIPE = 0>
+__global__ void __launch_bounds__(TL::THREADS, TL::MINW)
 gemm_x2f16_planar_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
                      size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
   constexpr int BM = TL::BM, BN = TL::BN, NT = TL::THREADS;
@@ -354,41 +409,74 @@ gemm_x2f16_planar_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, co
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{};
-  auto compute = [&](int b) {
-    f16x8 fb[2][TN];
+  auto load_b = [&](int b, f16x8 (&y)[2][TN]) {
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[p][j] = *(const f16x8*)(sB(b, p) + boff + j * 16 * 32);
+      for (int j = 0; j < TN; ++j) y[p][j] = *(const f16x8*)(sB(b, p) + boff + j * 16 * 32);
+  };
+  auto load_a = [&](int b, int i, f16x8& x0, f16x8& x1) {
+    x0 = *(const f16x8*)(sA(b, 0) + aoff + i * 16 * 32);
+    x1 = *(const f16x8*)(sA(b, 1) + aoff + i * 16 * 32);
+  };
+  // one 16-row slice of the wave tile: a1*w0 + a0*w1 + a0*w0 (small terms first)
+  auto mma_row = [&](int i, const f16x8& x0, const f16x8& x1, const f16x8 (&y)[2][TN]) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const f16x8 a0 = *(const f16x8*)(sA(b, 0) + aoff + i * 16 * 32);
-      const f16x8 a1 = *(const f16x8*)(sA(b, 1) + aoff + i * 16 * 32);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        f32x4 c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, fb[0][j], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb[1][j], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb[0][j], c, 0, 0, 0);
-        acc[i][j] = c;
-      }
+    for (int j = 0; j < TN; ++j) {
+      f32x4 c = acc[i][j];
+      // W fragment as the A operand, activations as B: D = W A^T (see gemm_epilogue16t)
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(y[0][j], x1, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(y[1][j], x0, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(y[0][j], x0, c, 0, 0, 0);
+      acc[i][j] = c;
     }
   };
 
   const int nk = K / BK;
   issue(0, 0);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue((kt + 1) * BK, (kt + 1) & 1);
-    compute(kt & 1);
-    __syncthreads();
+  {
+    // PIPE 2 (diagnostics, tools/gemm_split_probe x2pt): per-wave cycles in the
+    // K loop, in the vmcnt(0) drain and in the barrier, to ep.stamps[4*block+wave/4..]
+    unsigned long long c_loop = 0, c_vm = 0, c_bar = 0, tl = 0;
+    if constexpr (PIPE == 2) tl = __builtin_amdgcn_s_memtime();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int b = kt & 1;
+      if (kt + 1 < nk) issue((kt + 1) * BK, b ^ 1);
+      f16x8 fb[2][TN];
+      load_b(b, fb);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        f16x8 x0, x1;
+        load_a(b, i, x0, x1);
+        mma_row(i, x0, x1, fb);
+      }
+      if constexpr (PIPE == 2) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        __syncthreads();
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        c_vm += t1 - t0;
+        c_bar += t2 - t1;
+      } else {
+        __syncthreads();
+      }
+    }
+    if constexpr (PIPE == 2) {
+      c_loop = __builtin_amdgcn_s_memtime() - tl;
+      if (lane == 0 && (wave == 0 || wave == NT / 64 - 1)) {
+        unsigned long long* o = ep.stamps + 6 * blockIdx.x + (wave ? 3 : 0);
+        o[0] = c_loop; o[1] = c_vm; o[2] = c_bar;
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] *= acc_scale;
-  gemm_epilogue16<EPI, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lane);
-  if (ep.stamps && t == 0) {
+  gemm_epilogue16t<EPI, VEC, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lane);
+  if (PIPE != 2 && ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
   }

@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     hipMalloc(&C, sizeof(float) * (size_t)s.M * s.N);
     hipMalloc(&flag, 8);
     hipMalloc(&wmax_bits, 8);
-    hipMalloc(&stamps, sizeof(unsigned long long) * 2 * maxgrid);
+    hipMalloc(&stamps, sizeof(unsigned long long) * 6 * maxgrid);
     hipMemset(flag, 0, 8);
     hipMemset(wmax_bits, 0, 8);
     hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, A, (size_t)s.M * s.K, 11u, s.gelu ? 3.0f : 1.0f, s.gelu);
@@ -105,6 +105,32 @@ int main(int argc, char** argv) {
           grid = gemm_x3_grid<X3Large>(s.M, s.N);
           hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS, X3Large>), dim3(grid), dim3(X3Large::THREADS), 0, 0,
                              A, s.K, W3, s.K, (size_t)s.N * s.K, s.M, s.N, s.K, ee);
+        } else if (path == "x2pt") {
+          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large, true, 2>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2pg") {  // the engine's QKV+MLP-in epilogue: bias, GELU, split planes
+          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          GemmEpi eg = ee;
+          eg.n_split = (s.N * 3 / 7) & ~3;  // ~3d of 3d + d_mlp
+          eg.out1h = (uint16_t*)(C) + eg.n_split;  // reuse C: row stride 2N halves (bytes of the fp32 row)
+          eg.ld1h = 2 * s.N;
+          eg.ps1h = s.N;
+          eg.range_flag = flag;
+          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_SPLIT_GELU_X2, X2Large, true, 0>), dim3(grid), dim3(X2Large::THREADS),
+                             0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+        } else if (path == "x2w0" || path == "x2w1") {
+          grid = gemm_x2_grid<X2Wide>(s.M, s.N);
+          if (path == "x2w0")
+            hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Wide, true, 0>), dim3(grid), dim3(X2Wide::THREADS), 0, 0,
+                               A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+          else
+            hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Wide, true, 0>), dim3(grid), dim3(X2Wide::THREADS), 0, 0,
+                               A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2p0") {
+          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large, true, 0>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2p") {
           grid = gemm_x2_grid<X2Large>(s.M, s.N);
           hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
@@ -115,6 +141,25 @@ int main(int argc, char** argv) {
                              A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
         }
       };
+      if (path == "x2pt") {  // K-loop anatomy: waves 0 and 7, medians over blocks
+        run(true);
+        hipDeviceSynchronize();
+        std::vector<unsigned long long> hs(6 * (size_t)grid);
+        hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost);
+        for (int w = 0; w < 2; ++w) {
+          std::vector<double> fv, fb;
+          for (int g = 0; g < grid; ++g) {
+            const double L = (double)hs[6 * g + 3 * w];
+            if (L > 0) { fv.push_back(hs[6 * g + 3 * w + 1] / L); fb.push_back(hs[6 * g + 3 * w + 2] / L); }
+          }
+          std::sort(fv.begin(), fv.end());
+          std::sort(fb.begin(), fb.end());
+          printf("{\"shape\": \"%s\", \"path\": \"x2pt\", \"wave\": %d, \"vmcnt_wait_frac\": %.3f, "
+                 "\"barrier_wait_frac\": %.3f}\n", s.name, w ? 7 : 0, fv[fv.size() / 2], fb[fb.size() / 2]);
+        }
+        fflush(stdout);
+        continue;
+      }
       run(false); hipDeviceSynchronize();
       hipEventRecord(a); run(false); hipEventRecord(b); hipEventSynchronize(b);
       float ms1; hipEventElapsedTime(&ms1, a, b);

@@ -21,7 +21,8 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout"}
+VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout", "3": "qkv_mlpin"}
+SIMDS = 1024  # 256 CUs x 4
 
 
 def one(d, pattern):
@@ -35,7 +36,7 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16"}
+FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16", "gemm_x2f16_planar_kernel": "x2f16"}
 
 
 def gemm_variant(name):
@@ -53,12 +54,55 @@ def pmc(d):
     return rows
 
 
+def mfma_util(rows):
+    """MFMA utilisation of the GEMM dispatches: SQ_VALU_MFMA_BUSY_CYCLES (summed
+    over every SIMD) / (SIMDs x shader cycles), shader cycles = GRBM_GUI_ACTIVE / 8
+    (rocprofv3 sums it over the 8 XCDs; MI355X_MICROARCH.md DVFS note); the
+    effective clock is those cycles over the dispatch's wall time.  SQ wave
+    states (quad-cycles) as fractions of SQ_WAVE_CYCLES."""
+    by = {}
+    for r in rows:
+        gv = gemm_variant(r["Kernel_Name"])
+        if not gv:
+            continue
+        d = by.setdefault((r["Dispatch_Id"], gv), {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    per = {}
+    for (_, (fam, v)), d in by.items():
+        p = per.setdefault(VARIANTS[v], {"launches": 0, "busy": 0.0, "grbm": 0.0, "ns": 0,
+                                         "wave": 0.0, "wait": 0.0, "wait_inst": 0.0, "active": 0.0})
+        p["launches"] += 1
+        p["busy"] += d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        p["grbm"] += d.get("GRBM_GUI_ACTIVE", 0.0)
+        p["ns"] += d["ns"]
+        p["wave"] += d.get("SQ_WAVE_CYCLES", 0.0)
+        p["wait"] += d.get("SQ_WAIT_ANY", 0.0)
+        p["wait_inst"] += d.get("SQ_WAIT_INST_ANY", 0.0)
+        p["active"] += d.get("SQ_ACTIVE_INST_ANY", 0.0)
+    def fmt(p):
+        cyc = p["grbm"] / 8
+        out = {"launches": p["launches"], "mfma_util": round(p["busy"] / (SIMDS * cyc), 4) if cyc else None,
+               "clock_mhz": round(cyc / (p["ns"] * 1e-9) / 1e6) if p["ns"] else None}
+        if p["wave"]:
+            out.update({"wave_wait_any": round(p["wait"] / p["wave"], 3),
+                        "wave_wait_inst": round(p["wait_inst"] / p["wave"], 3),
+                        "wave_active_inst": round(p["active"] / p["wave"], 3)})
+        return out
+    tot = {k: sum(p[k] for p in per.values()) for k in ("launches", "busy", "grbm", "ns", "wave", "wait",
+                                                          "wait_inst", "active")}
+    res = {"basis": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); clock = "
+                    "GRBM_GUI_ACTIVE / 8 / dispatch time", "all": fmt(tot)}
+    res["variants"] = {k: fmt(p) for k, p in per.items()}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
     ap.add_argument("--stats", required=True)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--mfma", help="PMC pass with SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE and the SQ wave states")
     ap.add_argument("--bench", help="bench.py JSON of the same command (algorithmic bytes per launch)")
     ap.add_argument("--cmd", default="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg")
     ap.add_argument("--out", default=str(ROOT / "profiles"), help="summary directory")
@@ -111,6 +155,8 @@ def main():
             pm["alg_bytes_per_launch"] = alg
             pm["workload"] = b["config"]["workload"]
             pm["ratio_hbm_to_alg"] = round(hbm / n / alg, 2)
+        if a.mfma:
+            pm["mfma"] = mfma_util(pmc(a.mfma))
         summary["pmc_gemm"] = pm
         (out_dir / f"pmc_gemm_{fam}.json").write_text(json.dumps(pm, indent=1) + "\n")
     (out_dir / f"rocprof_{a.tag}.json").write_text(json.dumps(summary, indent=1) + "\n")
