@@ -62,7 +62,6 @@ struct X2TileT {
 };
 using X2Large = X2TileT<256, 256, 2, 4>;  // 8 waves of 128x64, 128 KB LDS
 using X2Small = X2TileT<128, 128, 2, 2>;  // 4 waves of 64x64, 64 KB LDS
-using X2Wide = X2TileT<256, 256, 2, 2, 1>;  // 4 waves of 128x128, one per SIMD (512-VGPR budget), 128 KB LDS
 
 // One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land
 // at lds_base + 16 l.  (A non-template wrapper: referenced directly from a

@@ -2,7 +2,10 @@
 // paths (fp32 MFMA, 3-plane bf16 split, 2-plane fp16 split) at the engine's
 // real shapes, each checked against an fp64 reference on sampled rows.
 //   hipcc --offload-arch=gfx950 -O3 -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
-//   tools/gemm_split_probe [f32|x3|x2|x2p ...]   (default: all; x2p = x2 with A pre-split)
+//   tools/gemm_split_probe [f32|x3|x2|x2p|x2pg|x2pt ...]   (default: f32 x3 x2 x2p)
+//     x2p  = the engine's planar kernel (A pre-split, LDS-DMA, 16x16x32, EPI_BIAS)
+//     x2pg = the same with the QKV+MLP-in epilogue (bias, GELU, split-plane stores)
+//     x2pt = K-loop anatomy (cycles in vmcnt drain / barrier, waves 0 and 7)
 // A is drawn N(0,1) (a LayerNorm output) or GELU(3 N(0,1)) (the MLP-out input:
 // many tiny values, which exercises the fp16 residual plane's range).
 #include <hip/hip_runtime.h>
@@ -119,18 +122,6 @@ int main(int argc, char** argv) {
           eg.range_flag = flag;
           hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_SPLIT_GELU_X2, X2Large, true, 0>), dim3(grid), dim3(X2Large::THREADS),
                              0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
-        } else if (path == "x2w0" || path == "x2w1") {
-          grid = gemm_x2_grid<X2Wide>(s.M, s.N);
-          if (path == "x2w0")
-            hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Wide, true, 0>), dim3(grid), dim3(X2Wide::THREADS), 0, 0,
-                               A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-          else
-            hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Wide, true, 0>), dim3(grid), dim3(X2Wide::THREADS), 0, 0,
-                               A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2p0") {
-          grid = gemm_x2_grid<X2Large>(s.M, s.N);
-          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large, true, 0>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
-                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2p") {
           grid = gemm_x2_grid<X2Large>(s.M, s.N);
           hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
