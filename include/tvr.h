@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 3
+#define TVR_ABI_VERSION 4
 
 enum tvr_status {
   TVR_OK = 0,
@@ -130,11 +130,16 @@ int tvr_model_destroy(tvr_model* model);
  *                    attention mixes and GELU outputs of any Pythia do); a
  *                    launch that sees a larger one is reported by
  *                    tvr_model_range_status.
+ *   TVR_GEMM_BF16    bf16 weights and GEMM inputs on v_mfma_f32_16x16x32_bf16,
+ *                    fp32 accumulation (the north star's bf16 configuration,
+ *                    tolerance 2e-2; NOT fp32-accurate); weights 2 B/param.
  * Measured errors of both split modes against fp64 are at or below the fp32
  * MFMA GEMM's.  TransformerLens runs its matmuls in fp32
- * (scratch2.py:26 loads the default dtype); all three modes meet that.  The
- * planes are built on the device once.  Synchronises `stream`. */
-enum tvr_gemm_mode { TVR_GEMM_F32 = 0, TVR_GEMM_X3BF16 = 1, TVR_GEMM_X2F16 = 2 };
+ * (scratch2.py:26 loads the default dtype); F32, X3BF16 and X2F16 meet that.
+ * Everything outside the GEMMs (LayerNorm, attention, residual stream,
+ * softmax) is fp32 in every mode.  The planes are built on the device once.
+ * Synchronises `stream`. */
+enum tvr_gemm_mode { TVR_GEMM_F32 = 0, TVR_GEMM_X3BF16 = 1, TVR_GEMM_X2F16 = 2, TVR_GEMM_BF16 = 3 };
 int tvr_model_set_gemm(tvr_model* model, int32_t mode, void* stream);
 int32_t tvr_model_get_gemm(const tvr_model* model);
 /* TVR_OK, or TVR_ERR_RANGE if an X2F16 GEMM enqueued since the last call saw
@@ -201,28 +206,32 @@ int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream);
 int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
                     size_t wps, const float* bias, float* C, int32_t ldc,
                     int32_t M, int32_t N, int32_t K, void* stream);
-/* Split W [n] fp32 into 2 fp16 planes out [2][n] of w * scale (uint16
- * storage); scale is a power of two (X2F16 mode picks 2^(15 - ceil log2 max|W|)). */
-int tvr_split_planes_f16(const float* w, float scale, uint16_t* out, size_t n, void* stream);
-/* tvr_gemm_f32 on the 2-plane fp16 operand: W planes [2][.][ldw] (plane stride
- * wps) built with scale w_scale.  *range_flag (device, may be NULL) is or-ed
- * with 1 if |A| reaches the split's range limit. */
+/* Weight planes of a planar mode (fmt = TVR_GEMM_X2F16 or TVR_GEMM_BF16):
+ * X2F16 two fp16 planes out [2][n] of w * scale (scale a power of two; the
+ * engine uses 2^(15 - ceil log2 max|W|)), BF16 one bf16 plane out [n]. */
+int tvr_weight_planes(int32_t fmt, const float* w, float scale, uint16_t* out, size_t n,
+                      void* stream);
+/* tvr_gemm_f32 with the split happening inside the GEMM: A fp32, W planes
+ * [2][.][ldw] (plane stride wps) from tvr_weight_planes(TVR_GEMM_X2F16, ..,
+ * w_scale, ..).  *range_flag (device, may be NULL) is or-ed with 1 if |A|
+ * reaches the split's range limit. */
 int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
                    size_t wps, float w_scale, const float* bias, float* C,
                    int32_t ldc, int32_t M, int32_t N, int32_t K,
                    uint32_t* range_flag, void* stream);
-/* The X2F16 activation format the engine's producers write for every GEMM
- * input: logical [rows][K] -> halves [rows][2][K] (plane 0 = fp16(16 a),
- * plane 1 = fp16(16 a - plane 0)); *range_flag (may be NULL) |= 1 if
- * |a| >= 4095. */
-int tvr_split_rows_f16(const float* a, int32_t lda, uint16_t* out, int32_t rows,
-                       int32_t K, uint32_t* range_flag, void* stream);
-/* The engine's X2F16 GEMM: A in the activation format above (lda logical
- * elements per row, >= K), W planes as tvr_split_planes_f16 builds them. */
-int tvr_gemm_x2f16_planar(const uint16_t* A, int32_t lda, const uint16_t* W,
-                          int32_t ldw, size_t wps, float w_scale,
-                          const float* bias, float* C, int32_t ldc, int32_t M,
-                          int32_t N, int32_t K, void* stream);
+/* The activation format the engine's producers write for every GEMM input in
+ * a planar mode: logical [rows][K] -> halves [rows][2][K]; X2F16: plane 0 =
+ * fp16(16 a), plane 1 = fp16(16 a - plane 0), *range_flag (may be NULL) |= 1
+ * if |a| >= 4095; BF16: plane 0 = bf16(a). */
+int tvr_act_rows(int32_t fmt, const float* a, int32_t lda, uint16_t* out, int32_t rows,
+                 int32_t K, uint32_t* range_flag, void* stream);
+/* The engine's planar GEMM: A in the activation format above (lda logical
+ * elements per row, >= K), W planes from tvr_weight_planes (w_scale: the
+ * X2F16 scale, 1 for BF16). */
+int tvr_gemm_planar(int32_t fmt, const uint16_t* A, int32_t lda, const uint16_t* W,
+                    int32_t ldw, size_t wps, float w_scale, const float* bias,
+                    float* C, int32_t ldc, int32_t M, int32_t N, int32_t K,
+                    void* stream);
 /* TransformerLens LayerNormPre over rows: (x - mean) / sqrt(var + eps) */
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy,
                   int32_t rows, int32_t d, float eps, void* stream);
@@ -243,8 +252,8 @@ int tvr_profile_enable(tvr_model* model, int32_t on);
 int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);
- * the split-mode weight planes are not included (X3BF16 6 B, X2F16 4 B per
- * GEMM weight). */
+ * the weight planes of the split / bf16 modes are not included (X3BF16 6 B,
+ * X2F16 4 B, BF16 2 B per GEMM weight). */
 size_t tvr_workspace_bytes(const tvr_model* model);
 
 #ifdef __cplusplus

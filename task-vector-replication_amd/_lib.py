@@ -57,10 +57,10 @@ class CKernelStats(ctypes.Structure):
 GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 3  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 4  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
-GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2}
+GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
 
 SIGNATURES = {
     "tvr_version": (ctypes.c_char_p, []),
@@ -95,17 +95,18 @@ SIGNATURES = {
                                        ctypes.c_size_t, c_f32p, c_f32p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "tvr_model_range_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
-    "tvr_split_planes_f16": (ctypes.c_int, [c_f32p, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
-                                            ctypes.c_void_p]),
+    "tvr_weight_planes": (ctypes.c_int, [ctypes.c_int32, c_f32p, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]),
     "tvr_gemm_x2f16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
                                       ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p, ctypes.c_int32,
                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p]),
-    "tvr_split_rows_f16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
-                                          ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
-    "tvr_gemm_x2f16_planar": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
-                                             ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p, ctypes.c_int32,
-                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
+    "tvr_act_rows": (ctypes.c_int, [ctypes.c_int32, c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                    ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
+    "tvr_gemm_planar": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_int32, ctypes.c_size_t, ctypes.c_float, c_f32p, c_f32p,
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p]),
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
 }

@@ -19,6 +19,7 @@
 
 #include "tvr.h"
 #include "gemm_f32.hpp"
+#include "gemm_planar.hpp"
 #include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
 #include "kernels.hpp"
@@ -72,8 +73,9 @@ struct Staging {
 };
 
 // A GEMM weight operand: the fp32 matrix and, in a split mode, its planes
-// (plane stride wps elements): TVR_GEMM_X3BF16 three bf16 planes in x,
-// TVR_GEMM_X2F16 two fp16 planes of w * wscale in h.
+// (plane stride wps elements): TVR_GEMM_X3BF16 three bf16 planes in x;
+// the planar modes in h: TVR_GEMM_X2F16 two fp16 planes of w * wscale,
+// TVR_GEMM_BF16 one bf16 plane.
 struct MatW {
   const float* f = nullptr;
   const uint16_t* x = nullptr;
@@ -206,19 +208,28 @@ hipEvent_t prof_event(tvr_model* m) {
   return e;
 }
 
-// C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] or, with a_split, the
-// X2F16 activation format (split.hpp: lda logical elements per row); split A
-// needs the X2F16 weight planes (W.h) and runs the LDS-DMA planar kernel.
-int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, int ldw, int M, int N,
+// Activation format of the model's GEMM inputs (split.hpp).
+int act_fmt(const tvr_model* m) {
+  return m->gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : m->gemm_mode == TVR_GEMM_BF16 ? ACT_BF16 : ACT_F32;
+}
+
+// C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] (a_fmt ACT_F32) or a
+// planar activation format (split.hpp: lda logical elements per row), which
+// needs the same format's weight planes (W.h) and runs gemm_planar_kernel.
+int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int ldw, int M, int N,
                 int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr,
                 unsigned* range_flag = nullptr) {
   if (M <= 0 || N <= 0) return TVR_OK;
-  if (a_split && !W.h) return fail(TVR_ERR_INVALID, "gemm: split activations need the X2F16 weight planes");
-  if (epi == EPI_SPLIT_GELU_X2 && !a_split)
-    return fail(TVR_ERR_INVALID, "gemm: the split-GELU epilogue belongs to the X2F16 path");
-  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0))
-    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes; K=" +
-                                         std::to_string(K) + ")");
+  const bool planar = a_fmt != ACT_F32;
+  if (planar && !W.h) return fail(TVR_ERR_INVALID, "gemm: planar activations need the planar weight planes");
+  if (epi == EPI_SPLIT_GELU_ACT && !planar)
+    return fail(TVR_ERR_INVALID, "gemm: the activation-format GELU epilogue belongs to the planar paths");
+  if (epi == EPI_SPLIT_GELU && planar)
+    return fail(TVR_ERR_INVALID, "gemm: planar paths write GELU columns in their activation format");
+  if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0) ||
+      (a_fmt == ACT_BF16 && K % 64 != 0))
+    return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes, K of 64 for "
+                                     "bf16; K=" + std::to_string(K) + ")");
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (m && m->prof) {
     ev0 = prof_event(m);
@@ -233,97 +244,113 @@ int launch_gemm(int epi, const void* A, int lda, bool a_split, const MatW& W, in
   hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
                      0, st, Af, lda, W.x, ldw, W.wps, M, N, K, ep)
   unsigned* flag = m ? m->range_flag : range_flag;
-  const float acc_scale = 1.0f / (W.wscale * X2_ASCALE);
+  const float acc_scale = (a_fmt == ACT_BF16) ? 1.0f : 1.0f / (W.wscale * X2_ASCALE);
   const float* Af = static_cast<const float*>(A);
   const uint16_t* Ah = static_cast<const uint16_t*>(A);
-  const bool vec = x2_epilogue_vec(epi, ep, N);
-#define TVR_X2P_LAUNCH1(E, TL, V)                                                                            \
-  hipLaunchKernelGGL((gemm_x2f16_planar_kernel<E, TL, V>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
+  const bool vec = planar_epilogue_vec(epi, ep, N);
+#define TVR_PL_LAUNCH2(E, TL, F, V)                                                                         \
+  hipLaunchKernelGGL((gemm_planar_kernel<E, TL, F, V>), dim3(gemm_planar_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
-#define TVR_X2P_LAUNCH(E, TL) \
-  if (vec) TVR_X2P_LAUNCH1(E, TL, true); else TVR_X2P_LAUNCH1(E, TL, false)
+#define TVR_PL_LAUNCH1(E, TL, F) \
+  if (vec) TVR_PL_LAUNCH2(E, TL, F, true); else TVR_PL_LAUNCH2(E, TL, F, false)
+#define TVR_PL_LAUNCH(E)                                                                               \
+  if (a_fmt == ACT_X2F16) {                                                                              \
+    if (large) { TVR_PL_LAUNCH1(E, PlanarLarge, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
+  } else {                                                                                               \
+    if (large) { TVR_PL_LAUNCH1(E, PlanarLarge, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
+  }
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Af, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
-#define TVR_GEMM_PICK(E)                                    \
-  if (a_split) {                                            \
-    if (large) { TVR_X2P_LAUNCH(E, X2Large); } else { TVR_X2P_LAUNCH(E, X2Small); }     \
-  } else if (W.h) {                                         \
+#define TVR_GEMM_PICK_NP(E)                                 \
+  if (W.h) {                                                \
     if (large) TVR_X2_LAUNCH(E, X2Large); else TVR_X2_LAUNCH(E, X2Small);         \
   } else if (W.x) {                                         \
     if (large) TVR_X3_LAUNCH(E, X3Large); else TVR_X3_LAUNCH(E, X3Small);         \
   } else {                                                  \
     if (large) TVR_GEMM_LAUNCH(E, TileLarge); else TVR_GEMM_LAUNCH(E, TileSmall); \
   }
+#define TVR_GEMM_PICK(E) \
+  if (planar) { TVR_PL_LAUNCH(E); } else { TVR_GEMM_PICK_NP(E); }
   switch (epi) {
     case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
-    case EPI_SPLIT_GELU: TVR_GEMM_PICK(EPI_SPLIT_GELU); break;
-    case EPI_SPLIT_GELU_X2:
-      if (large) { TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Large); } else { TVR_X2P_LAUNCH(EPI_SPLIT_GELU_X2, X2Small); }
-      break;
+    case EPI_SPLIT_GELU: TVR_GEMM_PICK_NP(EPI_SPLIT_GELU); break;
+    case EPI_SPLIT_GELU_ACT: TVR_PL_LAUNCH(EPI_SPLIT_GELU_ACT); break;
     default: TVR_GEMM_PICK(EPI_RESID); break;
   }
 #undef TVR_GEMM_PICK
+#undef TVR_GEMM_PICK_NP
 #undef TVR_X3_LAUNCH
 #undef TVR_X2_LAUNCH
-#undef TVR_X2P_LAUNCH
-#undef TVR_X2P_LAUNCH1
+#undef TVR_PL_LAUNCH
+#undef TVR_PL_LAUNCH1
+#undef TVR_PL_LAUNCH2
 #undef TVR_GEMM_LAUNCH
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
-    const double wbytes = W.x ? 6.0 : 4.0;  // W read once per launch: fp32, 3 bf16 or 2 fp16 planes
-    m->prof_recs.push_back({ev0, ev1, epi == EPI_SPLIT_GELU_X2 ? (int)EPI_SPLIT_GELU : epi, 2.0 * M * N * (double)K,
-                            4.0 * ((double)M * K + (double)M * N) + wbytes * N * (double)K});
+    // minimal operand bytes: W read once (fp32 4, 3 bf16 planes 6, 2 fp16 planes 4, bf16 2 B per element),
+    // A once in its format (fp32 / x2f16 4, bf16 2), C once as fp32
+    const double wbytes = W.x ? 6.0 : (a_fmt == ACT_BF16 ? 2.0 : 4.0);
+    const double abytes = a_fmt == ACT_BF16 ? 2.0 : 4.0;
+    m->prof_recs.push_back({ev0, ev1, epi == EPI_SPLIT_GELU_ACT ? (int)EPI_SPLIT_GELU : epi, 2.0 * M * N * (double)K,
+                            abytes * M * (double)K + 4.0 * M * (double)N + wbytes * N * (double)K});
   }
   return TVR_OK;
 }
 
-// y: fp32 [rows][ldy] or (split) the X2F16 activation format
+// y: fp32 [rows][ldy] (ACT_F32) or a planar activation format
 int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
-                 int d, float eps, bool split, hipStream_t st) {
+                 int d, float eps, int fmt, hipStream_t st) {
   if (rows <= 0) return TVR_OK;
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
     return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
-  if (split)
-    hipLaunchKernelGGL(lnpre_kernel<true>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+  if (fmt == ACT_X2F16)
+    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+  else if (fmt == ACT_BF16)
+    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
   else
-    hipLaunchKernelGGL(lnpre_kernel<false>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
 
-// Activation buffers of one launch sequence.  In X2F16 mode (`split`) xn and
-// a2 hold the split fp16 activation format (split.hpp), same bytes.
+// Activation buffers of one launch sequence.  In the planar modes xn and a2
+// hold the model's activation format `fmt` (split.hpp) in the same bytes.
 struct Acts {
   float* resid;   // [R][d]
   float* xn;      // [R][d]
   float* qkv;     // [R][3d]
   float* a2;      // [R][K2]  (z | gelu(mlp-in))
-  bool split;
+  int fmt;
 };
 
-// z: the z columns of a2 (fp32, or split); zf: optional fp32 copy [rows][d]
+// z: the z columns of a2 (fp32 or activation format fmt); zf: optional fp32 copy [rows][d]
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
-                     int n_seqs, int maxT, void* z, bool split, float* zf, hipStream_t st) {
+                     int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const size_t smem = attention_smem_bytes(maxT, c.d_head);
-  const void* kern = split ? (const void*)attention_kernel<true> : (const void*)attention_kernel<false>;
-  if (smem > 64 * 1024)
-    TVR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
   const float inv_scale = 1.0f / std::sqrt((float)c.d_head);
-  if (split)
-    hipLaunchKernelGGL(attention_kernel<true>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
-                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,
-                       c.d_head, c.rotary_dim, inv_scale);
+#define TVR_ATT_LAUNCH(F)                                                                                     \
+  do {                                                                                                        \
+    if (smem > 64 * 1024)                                                                                     \
+      TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)smem));                                                                \
+    hipLaunchKernelGGL(attention_kernel<F>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,    \
+                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,     \
+                       c.d_head, c.rotary_dim, inv_scale);                                                    \
+  } while (0)
+  if (fmt == ACT_X2F16)
+    TVR_ATT_LAUNCH(ACT_X2F16);
+  else if (fmt == ACT_BF16)
+    TVR_ATT_LAUNCH(ACT_BF16);
   else
-    hipLaunchKernelGGL(attention_kernel<false>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,
-                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,
-                       c.d_head, c.rotary_dim, inv_scale);
+    TVR_ATT_LAUNCH(ACT_F32);
+#undef TVR_ATT_LAUNCH
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
@@ -332,15 +359,16 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
 //   x = LNPre(resid); [qkv | h] = x @ W1^T + b1; z = attn(qkv); resid += [z|gelu h] @ W2^T + b2
 // (run_block computes up to z; run_block_out the second projection.)
 // The QKV+MLP-in epilogue: Q|K|V fp32 to qkv (row stride 3d), GELU(h) into
-// the a2 columns after z (fp32, or split).
+// the a2 columns after z (fp32, or the activation format).
 GemmEpi epi_qkv_mlpin(tvr_model* m, const float* b1, float* qkv, const Acts& a) {
+  const bool planar = a.fmt != ACT_F32;
   const int d = m->cfg.d_model;
   GemmEpi e{};
   e.bias = b1;
   e.out0 = qkv;
   e.ld0 = 3 * d;
   e.n_split = 3 * d;
-  if (a.split) {
+  if (planar) {
     e.out1h = reinterpret_cast<uint16_t*>(a.a2) + d;
     e.ld1h = 2 * m->K2;
     e.ps1h = m->K2;
@@ -357,11 +385,11 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.split, st));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st));
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
-  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split, m->w1[l], d, R, m->D1, d,
+  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, R, m->D1, d,
                       e1, st, m));
-  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.split, zf, st);
+  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st);
 }
 
 // The last layer when only each sequence's LAST row is read afterwards (patch
@@ -376,20 +404,20 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.split, st));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st));
   GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row (all below n_split: no GELU)
   kv.bias = w.b1 + d;
   kv.out0 = a.qkv + d;
   kv.ld0 = 3 * d;
   kv.n_split = 2 * d;
-  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split,
+  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt,
                       m->w1[l].rows((size_t)d * d), d, R, 2 * d, d, kv, st, m));
   GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);  // all columns for the last rows, gathered and scattered in place
   e1.a_rows = d_last;
   e1.out_rows = d_last;
-  TVR_TRY(launch_gemm(a.split ? EPI_SPLIT_GELU_X2 : EPI_SPLIT_GELU, a.xn, d, a.split, m->w1[l], d, n_last, m->D1,
+  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, n_last, m->D1,
                       d, e1, st, m));
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.split, zf, st));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
   e2.bias = w.b2;
@@ -399,7 +427,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e2.ldr = d;
   e2.a_rows = d_last;
   e2.out_rows = d_last;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, a.split, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
 }
 
 int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
@@ -411,24 +439,24 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
   e2.ld0 = d;
   e2.resid = a.resid;
   e2.ldr = d;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, a.split, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
 }
 
 // Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
 int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int32_t* d_targets,
               int n, float* xf, float* logits_ws, float* out_prob, int32_t* out_topk, int topk,
-              float* out_logits, bool split, hipStream_t st) {
+              float* out_logits, int fmt, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model, V = c.d_vocab;
   for (int s = 0; s < n; s += kFinalChunk) {
     const int cn = std::min(kFinalChunk, n - s);
-    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, split, st));
+    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st));
     float* lg = out_logits ? out_logits + (size_t)s * V : logits_ws;
     GemmEpi e{};
     e.bias = m->b_unembed;
     e.out0 = lg;
     e.ld0 = V;
-    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, split, m->wu, d, cn, V, d, e, st, m));
+    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, fmt, m->wu, d, cn, V, d, e, st, m));
     hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
                        d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
                        out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
@@ -458,7 +486,7 @@ int check_config(const tvr_config& c) {
 extern "C" {
 
 const char* tvr_version(void) {
-  return "tvr-mi355x 0.3.0 (gfx950, fp32 MFMA | fp32-accurate 3-plane bf16 / 2-plane fp16 split MFMA)";
+  return "tvr-mi355x 0.4.0 (gfx950, fp32 MFMA | fp32-accurate 3-plane bf16 / 2-plane fp16 split MFMA | bf16 MFMA)";
 }
 int32_t tvr_abi_version(void) { return TVR_ABI_VERSION; }
 const char* tvr_last_error(void) { return g_last_error.c_str(); }
@@ -543,9 +571,11 @@ int32_t tvr_model_get_gemm(const tvr_model* m) { return m ? m->gemm_mode : -1; }
 
 int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: null model");
-  if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16 && mode != TVR_GEMM_X2F16)
+  if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16 && mode != TVR_GEMM_X2F16 && mode != TVR_GEMM_BF16)
     return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: unknown mode " + std::to_string(mode));
   if (mode == m->gemm_mode) return TVR_OK;
+  if (mode == TVR_GEMM_BF16 && (m->cfg.d_model % 64 != 0 || m->K2 % 64 != 0))
+    return fail(TVR_ERR_UNSUPPORTED, "tvr_model_set_gemm: bf16 needs d_model and d_model + d_mlp multiples of 64");
   const hipStream_t st = (hipStream_t)stream;
   TVR_HIP(hipStreamSynchronize(st));
   // back to plain fp32 operands first (frees the previous mode's planes)
@@ -561,7 +591,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   const int L = c.n_layers;
   const size_t n1 = (size_t)m->D1 * c.d_model, n2 = (size_t)c.d_model * m->K2;
   const size_t nu = (size_t)c.d_vocab * c.d_model;
-  const int np = mode == TVR_GEMM_X3BF16 ? 3 : 2;
+  const int np = mode == TVR_GEMM_X3BF16 ? 3 : mode == TVR_GEMM_X2F16 ? 2 : 1;
   const size_t total = np * ((n1 + n2) * L + nu);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
@@ -606,6 +636,9 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     if (mode == TVR_GEMM_X3BF16) {
       hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
       w = MatW{w.f, p, nullptr, n, 1.0f};
+    } else if (mode == TVR_GEMM_BF16) {
+      hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
+      w = MatW{w.f, nullptr, p, n, 1.0f};
     } else {
       hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, st, w.f, scale[i], p, n);
       w = MatW{w.f, nullptr, p, n, scale[i]};
@@ -773,9 +806,9 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   ub.add(o_tg, tg);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
-  const bool split = m->gemm_mode == TVR_GEMM_X2F16;
+  const int fmt = act_fmt(m);
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), trace ? nullptr : (float*)(base + o_qkv),
-         (float*)(base + o_a2), split};
+         (float*)(base + o_a2), fmt};
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const int32_t* d_last = (const int32_t*)(base + o_last);
   const size_t tstride = trace ? (size_t)trace->max_tokens * d : 0;
@@ -821,7 +854,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   }
   if (out_prob || out_topk || out_logits)
     TVR_TRY(run_final(m, a.resid, d_last, (const int32_t*)(base + o_tg), n_seq, (float*)(base + o_xf),
-                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, split,
+                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt,
                       st));
   return TVR_OK;
 }
@@ -952,9 +985,9 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   ub.add(o_tg, tg);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
-  const bool split = m->gemm_mode == TVR_GEMM_X2F16;
+  const int fmt = act_fmt(m);
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), (float*)(base + o_qkv),
-         (float*)(base + o_a2), split};
+         (float*)(base + o_a2), fmt};
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const EntryDesc* d_ents = (const EntryDesc*)(base + o_ents);
   const size_t tstride = (size_t)trace->max_tokens * d;
@@ -992,7 +1025,7 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   TVR_TRY(enter(L));
   return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
                    (float*)(base + o_xf), out_logits ? nullptr : (float*)(base + o_lg), out_prob,
-                   out_topk, topk, out_logits, split, st);
+                   out_topk, topk, out_logits, fmt, st);
 }
 
 int tvr_project_heads(tvr_model* m, const float* zsum, float* out, void* stream) {
@@ -1012,7 +1045,7 @@ int tvr_gemm_f32(const float* A, int32_t lda, const float* W, int32_t ldw, const
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, false, MatW{W}, ldw, M, N, K, e, (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, ACT_F32, MatW{W}, ldw, M, N, K, e, (hipStream_t)stream);
 }
 
 int tvr_split_planes(const float* w, uint16_t* out, size_t n, void* stream) {
@@ -1031,14 +1064,18 @@ int tvr_gemm_x3bf16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw,
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, false, MatW{nullptr, W, nullptr, wps, 1.0f}, ldw, M, N, K, e,
+  return launch_gemm(EPI_BIAS, A, lda, ACT_F32, MatW{nullptr, W, nullptr, wps, 1.0f}, ldw, M, N, K, e,
                      (hipStream_t)stream);
 }
 
-int tvr_split_planes_f16(const float* w, float scale, uint16_t* out, size_t n, void* stream) {
-  if (!w || !out) return fail(TVR_ERR_INVALID, "tvr_split_planes_f16: null argument");
+int tvr_weight_planes(int32_t fmt, const float* w, float scale, uint16_t* out, size_t n, void* stream) {
+  if (!w || !out || (fmt != TVR_GEMM_X2F16 && fmt != TVR_GEMM_BF16))
+    return fail(TVR_ERR_INVALID, "tvr_weight_planes: bad argument");
   if (n == 0) return TVR_OK;
-  hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, scale, out, n);
+  if (fmt == TVR_GEMM_X2F16)
+    hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, scale, out, n);
+  else
+    hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, out, n);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
@@ -1053,39 +1090,43 @@ int tvr_gemm_x2f16(const float* A, int32_t lda, const uint16_t* W, int32_t ldw, 
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, false, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
+  return launch_gemm(EPI_BIAS, A, lda, ACT_F32, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
                      (hipStream_t)stream, nullptr, range_flag);
 }
 
-int tvr_split_rows_f16(const float* a, int32_t lda, uint16_t* out, int32_t rows, int32_t K, uint32_t* range_flag,
-                       void* stream) {
-  if (!a || !out || rows < 0 || K <= 0 || lda < K) return fail(TVR_ERR_INVALID, "tvr_split_rows_f16: bad argument");
+int tvr_act_rows(int32_t fmt, const float* a, int32_t lda, uint16_t* out, int32_t rows, int32_t K,
+                 uint32_t* range_flag, void* stream) {
+  if (!a || !out || rows < 0 || K <= 0 || lda < K || (fmt != TVR_GEMM_X2F16 && fmt != TVR_GEMM_BF16))
+    return fail(TVR_ERR_INVALID, "tvr_act_rows: bad argument");
   const size_t n = (size_t)rows * K;
   if (n == 0) return TVR_OK;
-  hipLaunchKernelGGL(split_rows_f16_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, a, lda, out, rows, K, range_flag);
+  const dim3 grid((unsigned)std::min<size_t>((n + 255) / 256, 8192)), block(256);
+  if (fmt == TVR_GEMM_X2F16)
+    hipLaunchKernelGGL(act_rows_kernel<ACT_X2F16>, grid, block, 0, (hipStream_t)stream, a, lda, out, rows, K, range_flag);
+  else
+    hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, grid, block, 0, (hipStream_t)stream, a, lda, out, rows, K, range_flag);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
 
-int tvr_gemm_x2f16_planar(const uint16_t* A, int32_t lda, const uint16_t* W, int32_t ldw, size_t wps,
-                          float w_scale, const float* bias, float* C, int32_t ldc, int32_t M, int32_t N, int32_t K,
-                          void* stream) {
+int tvr_gemm_planar(int32_t fmt, const uint16_t* A, int32_t lda, const uint16_t* W, int32_t ldw, size_t wps,
+                    float w_scale, const float* bias, float* C, int32_t ldc, int32_t M, int32_t N, int32_t K,
+                    void* stream) {
   if (!A || !W || !C || M < 0 || N < 0 || K <= 0 || lda < K || !(w_scale > 0.0f) ||
-      wps < (size_t)ldw * (N > 0 ? N - 1 : 0) + K)
-    return fail(TVR_ERR_INVALID, "tvr_gemm_x2f16_planar: bad argument");
+      (fmt != TVR_GEMM_X2F16 && fmt != TVR_GEMM_BF16) || wps < (size_t)ldw * (N > 0 ? N - 1 : 0) + K)
+    return fail(TVR_ERR_INVALID, "tvr_gemm_planar: bad argument");
   GemmEpi e{};
   e.bias = bias;
   e.out0 = C;
   e.ld0 = ldc;
-  return launch_gemm(EPI_BIAS, A, lda, true, MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e,
-                     (hipStream_t)stream);
+  return launch_gemm(EPI_BIAS, A, lda, fmt == TVR_GEMM_X2F16 ? ACT_X2F16 : ACT_BF16,
+                     MatW{nullptr, nullptr, W, wps, w_scale}, ldw, M, N, K, e, (hipStream_t)stream);
 }
 
 int tvr_lnpre_f32(const float* x, int32_t ldx, float* y, int32_t ldy, int32_t rows, int32_t d, float eps,
                   void* stream) {
   if (!x || !y || rows < 0 || d <= 0) return fail(TVR_ERR_INVALID, "tvr_lnpre_f32: bad argument");
-  return launch_lnpre(x, ldx, nullptr, y, ldy, rows, d, eps, false, (hipStream_t)stream);
+  return launch_lnpre(x, ldx, nullptr, y, ldy, rows, d, eps, ACT_F32, (hipStream_t)stream);
 }
 
 }  // extern "C"

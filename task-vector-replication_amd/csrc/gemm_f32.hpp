@@ -46,7 +46,7 @@ enum GemmEpiKind {
   EPI_BIAS = 0,        // out0 = acc + bias
   EPI_SPLIT_GELU = 1,  // col < n_split: out0 = acc + bias ; else out1 = gelu(acc + bias)
   EPI_RESID = 2,       // out0 = acc + bias + resid   (in place allowed: out0 == resid)
-  EPI_SPLIT_GELU_X2 = 3,  // EPI_SPLIT_GELU with the GELU columns stored as fp16 split planes (split.hpp)
+  EPI_SPLIT_GELU_ACT = 3,  // EPI_SPLIT_GELU with the GELU columns in the planar activation format (split.hpp)
 };
 
 struct GemmEpi {
@@ -62,7 +62,7 @@ struct GemmEpi {
   // a_rows[m], output row m (and its residual) lives at out_rows[m].
   const int32_t* a_rows;
   const int32_t* out_rows;
-  // EPI_SPLIT_GELU_X2: GELU column c of row r goes to out1h + r*ld1h + c
+  // EPI_SPLIT_GELU_ACT: GELU column c of row r goes to out1h + r*ld1h + c
   // (plane 0) and + ps1h (plane 1), both in halves; range_flag as split.hpp.
   uint16_t* out1h;
   int ld1h;
@@ -78,8 +78,9 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-// One output element of the fused epilogues (v = acc + bias already).
-template <int EPI>
+// One output element of the fused epilogues (v = acc + bias already); FMT is
+// the activation format of EPI_SPLIT_GELU_ACT's GELU columns.
+template <int EPI, int FMT = ACT_X2F16>
 __device__ __forceinline__ void epi_store(const GemmEpi& ep, size_t orow, int col, float v) {
   if constexpr (EPI == EPI_BIAS) {
     ep.out0[orow * ep.ld0 + col] = v;
@@ -88,11 +89,11 @@ __device__ __forceinline__ void epi_store(const GemmEpi& ep, size_t orow, int co
       ep.out0[orow * ep.ld0 + col] = v;
     else
       ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
-  } else if constexpr (EPI == EPI_SPLIT_GELU_X2) {
+  } else if constexpr (EPI == EPI_SPLIT_GELU_ACT) {
     if (col < ep.n_split)
       ep.out0[orow * ep.ld0 + col] = v;
     else
-      store_split(ep.out1h + orow * ep.ld1h + (col - ep.n_split), ep.ps1h, gelu_erf(v), ep.range_flag);
+      store_act<FMT>(ep.out1h + orow * ep.ld1h + (col - ep.n_split), ep.ps1h, gelu_erf(v), ep.range_flag);
   } else {
     ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
   }

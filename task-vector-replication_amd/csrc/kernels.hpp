@@ -72,10 +72,10 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
 
 // ---------------------------------------------------------------------------
 // LayerNormPre (TL, after fold_ln): x -= mean(x); x /= sqrt(mean(x^2) + eps).
-// One wave per row; rows optionally gathered through `row_idx`.  SPLIT: y is
-// the X2F16 activation format (split.hpp; ldy counts logical elements); the
-// outputs are bounded by sqrt(d), so no range check.
-template <bool SPLIT>
+// One wave per row; rows optionally gathered through `row_idx`.  FMT: y is
+// fp32 (ACT_F32) or a planar activation format (split.hpp; ldy counts logical
+// elements); the outputs are bounded by sqrt(d), so no range check.
+template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
                              void* __restrict__ y, int ldy, int rows, int d,
@@ -103,11 +103,8 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     float4 v = xr[c];
     v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;
     v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
-    if constexpr (SPLIT) {
-      uint16_t* yr = (uint16_t*)y + (size_t)r * 2 * ldy + 4 * c;
-      const SplitF16 a = split_f16(v.x), b = split_f16(v.y), e = split_f16(v.z), f = split_f16(v.w);
-      *(uint2*)yr = make_uint2(a.h0 | ((unsigned)b.h0 << 16), e.h0 | ((unsigned)f.h0 << 16));
-      *(uint2*)(yr + ldy) = make_uint2(a.h1 | ((unsigned)b.h1 << 16), e.h1 | ((unsigned)f.h1 << 16));
+    if constexpr (FMT != ACT_F32) {
+      store_act4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, v.x, v.y, v.z, v.w, nullptr);
     } else {
       ((float4*)((float*)y + (size_t)r * ldy))[c] = v;
     }
@@ -124,7 +121,8 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
 // wave-shuffle softmax, one output dim per lane.
 //   qkv  [rows][3d]: q at h*dh, k at d + h*dh, v at 2d + h*dh (pre-rotary)
 //   z    [rows][ldz]: written at h*dh  (attn.hook_z), the next GEMM's input:
-//        fp32, or SPLIT: the X2F16 format (split.hpp), range-checked into flag
+//        fp32, or a planar activation format FMT (split.hpp; X2F16 is
+//        range-checked into flag)
 //   zf   [rows][ldzf] fp32 copy (trace / capture) or nullptr
 constexpr int ATT_THREADS = 256;
 constexpr int ATT_MAX_T = 128;
@@ -137,7 +135,7 @@ inline size_t attention_smem_bytes(int T, int dh) {
   return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
 }
 
-template <bool SPLIT>
+template <int FMT>
 __global__ void __launch_bounds__(ATT_THREADS)
 attention_kernel(const float* __restrict__ qkv, int ldq,
                  const float* __restrict__ cache, int ldc,
@@ -226,8 +224,8 @@ attention_kernel(const float* __restrict__ qkv, int ldq,
     for (int k = lane; k < dh; k += 64) {
       float a = 0.f;
       for (int j = 0; j <= pos; ++j) a += Ps[j] * Vs[j * dhp + k];
-      if constexpr (SPLIT)
-        store_split((uint16_t*)z + zrow * 2 * ldz + h * dh + k, ldz, a, flag);
+      if constexpr (FMT != ACT_F32)
+        store_act<FMT>((uint16_t*)z + zrow * 2 * ldz + h * dh + k, ldz, a, flag);
       else
         ((float*)z)[zrow * ldz + h * dh + k] = a;
       if (zf) zf[zrow * ldzf + h * dh + k] = a;

@@ -1,4 +1,8 @@
-// split.hpp — the activation side of the TVR_GEMM_X2F16 format.
+// split.hpp — activation formats of the planar GEMM paths.
+//
+// ACT_X2F16 (TVR_GEMM_X2F16), described below, and ACT_BF16 (TVR_GEMM_BF16):
+// bf16(a) in plane 0 of the same [R][2][K]-halves layout (plane 1 unused),
+// round to nearest even, no range limit.
 //
 // In X2F16 mode every GEMM input activation (LayerNorm outputs, attention z,
 // GELU(h)) is written by its producer as two fp16 planes of 16 * a, interleaved
@@ -14,6 +18,8 @@
 #include <stdint.h>
 
 namespace tvr {
+
+enum ActFmt { ACT_F32 = 0, ACT_X2F16 = 1, ACT_BF16 = 2 };
 
 constexpr float X2_ASCALE = 16.0f;
 constexpr float X2_FP16_OVERFLOW = 65520.0f;  // fp16(x) is inf from here (round to nearest)
@@ -36,14 +42,47 @@ __device__ __forceinline__ void store_split(uint16_t* p, int plane, float a, uns
   if (fabsf(a) * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
 }
 
-// fp32 rows a [rows][lda] -> the split format with K logical columns
-__global__ void split_rows_f16_kernel(const float* __restrict__ a, int lda, uint16_t* __restrict__ out, int rows,
-                                      int K, unsigned* __restrict__ flag) {
+__device__ __forceinline__ uint16_t bf16_bits(float a) { return __builtin_bit_cast(uint16_t, (__bf16)a); }
+
+// one element in activation format FMT (ACT_X2F16 / ACT_BF16)
+template <int FMT>
+__device__ __forceinline__ void store_act(uint16_t* p, int plane, float a, unsigned* flag) {
+  if constexpr (FMT == ACT_X2F16)
+    store_split(p, plane, a, flag);
+  else
+    p[0] = bf16_bits(a);
+}
+
+// four consecutive elements (p 8-B aligned)
+template <int FMT>
+__device__ __forceinline__ void store_act4(uint16_t* p, int plane, float a, float b, float c, float d,
+                                           unsigned* flag) {
+  if constexpr (FMT == ACT_X2F16) {
+    const SplitF16 x = split_f16(a), y = split_f16(b), z = split_f16(c), w = split_f16(d);
+    *(uint2*)p = make_uint2(x.h0 | ((unsigned)y.h0 << 16), z.h0 | ((unsigned)w.h0 << 16));
+    *(uint2*)(p + plane) = make_uint2(x.h1 | ((unsigned)y.h1 << 16), z.h1 | ((unsigned)w.h1 << 16));
+    const float m = fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
+    if (m * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
+  } else {
+    *(uint2*)p = make_uint2(bf16_bits(a) | ((unsigned)bf16_bits(b) << 16), bf16_bits(c) | ((unsigned)bf16_bits(d) << 16));
+  }
+}
+
+// fp32 rows a [rows][lda] -> activation format FMT with K logical columns
+template <int FMT>
+__global__ void act_rows_kernel(const float* __restrict__ a, int lda, uint16_t* __restrict__ out, int rows, int K,
+                                unsigned* __restrict__ flag) {
   const size_t n = (size_t)rows * K;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const size_t r = i / K, c = i % K;
-    store_split(out + r * 2 * K + c, K, a[r * lda + c], flag);
+    store_act<FMT>(out + r * 2 * K + c, K, a[r * lda + c], flag);
   }
+}
+
+// W [n] fp32 -> one bf16 plane (TVR_GEMM_BF16 weights, load time)
+__global__ void bf16_plane_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = bf16_bits(w[i]);
 }
 
 }  // namespace tvr

@@ -141,9 +141,11 @@ class Model(TokenizerMixin):
         planes; inputs must stay below 4095 in magnitude, checked on the device
         after every engine call); ``"x3bf16"`` — fp32-accurate three-plane bf16
         split (six products, 6 B per weight, no range limit); ``"f32"`` —
-        ``v_mfma_f32_32x32x2_f32`` on the fp32 weights.  Both splits measure at
-        or below the fp32 MFMA GEMM's error against fp64.
-        Everything outside the GEMMs is fp32 in all three."""
+        ``v_mfma_f32_32x32x2_f32`` on the fp32 weights; ``"bf16"`` — bf16
+        weights and GEMM inputs, fp32 accumulation (NOT fp32-accurate: the
+        north star's bf16 configuration, 2e-2 tolerance).  Both splits measure
+        at or below the fp32 MFMA GEMM's error against fp64 (DESIGN.md
+        section 3).  Everything outside the GEMMs is fp32 in all four."""
         if mode not in _lib.GEMM_MODES:
             raise ValueError(f"gemm mode must be one of {sorted(_lib.GEMM_MODES)}, got {mode!r}")
         with torch.cuda.device(self.device):

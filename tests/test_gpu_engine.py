@@ -19,6 +19,7 @@ from oracle import reference_experiments as R
 pytestmark = pytest.mark.gpu
 
 ARROW = tvr_amd.tasks.ARROW
+X2F16, BF16 = tvr_amd._lib.GEMM_MODES["x2f16"], tvr_amd._lib.GEMM_MODES["bf16"]
 
 
 def rel_err(a, b):
@@ -93,7 +94,7 @@ def test_gemm_x2f16_matches_torch(M, N, K):
     e = int(np.frexp(W.abs().max().item())[1])
     scale = float(2.0 ** (15 - e))
     planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
-    tvr_amd._lib.check(lib.tvr_split_planes_f16(Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
+    tvr_amd._lib.check(lib.tvr_weight_planes(X2F16, Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
     # the planes sum back to W * scale within 2^-22 relative, or half the fp16
     # subnormal spacing (2^-25) where the residual plane is subnormal
     hp = planes.view(torch.float16).double()
@@ -124,25 +125,53 @@ def test_gemm_x2f16_planar_matches_torch(M, N, K):
     Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
     scale = float(2.0 ** (15 - int(np.frexp(W.abs().max().item())[1])))
     planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
-    tvr_amd._lib.check(lib.tvr_split_planes_f16(Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
+    tvr_amd._lib.check(lib.tvr_weight_planes(X2F16, Wd.data_ptr(), scale, planes.data_ptr(), N * K, st), "split")
     lda = K + 32  # a padded logical row: the format's stride is independent of K
     Ap = torch.zeros(M, lda, device="cuda")
     Ap[:, :K] = Ad
     Ah = torch.empty(M, 2, lda, dtype=torch.int16, device="cuda")
     flag = torch.zeros(1, dtype=torch.int32, device="cuda")
-    tvr_amd._lib.check(lib.tvr_split_rows_f16(Ap.data_ptr(), lda, Ah.data_ptr(), M, lda, flag.data_ptr(), st),
+    tvr_amd._lib.check(lib.tvr_act_rows(X2F16, Ap.data_ptr(), lda, Ah.data_ptr(), M, lda, flag.data_ptr(), st),
                        "split rows")
     # plane 0 + plane 1 = 16 a within 2^-22 relative (+ half the fp16 subnormal spacing)
     hs = Ah.view(torch.float16).double().sum(1)[:, :K]
     assert ((hs - 16 * Ad.double()).abs() <= 2.0 ** -22 * 16 * Ad.double().abs() + 2.0 ** -25).all()
     C = torch.empty(M, N, device="cuda")
-    tvr_amd._lib.check(lib.tvr_gemm_x2f16_planar(Ah.data_ptr(), lda, planes.data_ptr(), K, N * K, scale,
+    tvr_amd._lib.check(lib.tvr_gemm_planar(X2F16, Ah.data_ptr(), lda, planes.data_ptr(), K, N * K, scale,
                                                  bd.data_ptr(), C.data_ptr(), N, M, N, K, st), "gemm_x2p")
     ref = A.double() @ W.double().T + b.double()
     err = (C.cpu().double() - ref).abs().max().item()
     bound = 4e-7 * (A.double().abs() @ W.double().abs().T).max().item() + 1e-6
     assert err <= bound, (err, bound)
     assert flag.item() == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 64), (37, 130, 64), (300, 257, 320), (1000, 2560, 2560),
+                                   (129, 50304, 64), (3001, 17920, 128), (600, 2560, 12800)])
+def test_gemm_bf16_planar_matches_torch(M, N, K):
+    """The bf16 planar GEMM equals an fp64 GEMM of the bf16-rounded operands
+    up to fp32 accumulation error (the bf16 rounding itself is the mode)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 13 + N)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 2e-2
+    b = torch.randn(N, generator=g)
+    lib = tvr_amd._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    Ad, Wd, bd = A.cuda(), W.cuda(), b.cuda()
+    plane = torch.empty(N, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_weight_planes(BF16, Wd.data_ptr(), 1.0, plane.data_ptr(), N * K, st), "bf16 W")
+    assert torch.equal(plane.view(torch.bfloat16), Wd.to(torch.bfloat16))
+    Ah = torch.empty(M, 2, K, dtype=torch.int16, device="cuda")
+    tvr_amd._lib.check(lib.tvr_act_rows(BF16, Ad.data_ptr(), K, Ah.data_ptr(), M, K, None, st), "bf16 A")
+    assert torch.equal(Ah[:, 0].view(torch.bfloat16), Ad.to(torch.bfloat16))
+    C = torch.empty(M, N, device="cuda")
+    tvr_amd._lib.check(lib.tvr_gemm_planar(BF16, Ah.data_ptr(), K, plane.data_ptr(), K, N * K, 1.0, bd.data_ptr(),
+                                           C.data_ptr(), N, M, N, K, st), "gemm_bf16")
+    Ab, Wb = Ad.to(torch.bfloat16).double().cpu(), Wd.to(torch.bfloat16).double().cpu()
+    ref = Ab @ Wb.T + b.double()
+    err = (C.cpu().double() - ref).abs().max().item()
+    bound = 4e-7 * (Ab.abs() @ Wb.abs().T).max().item() + 1e-6
+    assert err <= bound, (err, bound)
 
 
 def test_gemm_x2f16_range_flag():
@@ -153,7 +182,7 @@ def test_gemm_x2f16_range_flag():
     A = torch.randn(M, K, device="cuda")
     W = torch.randn(N, K, device="cuda") * 0.02
     planes = torch.empty(2, N, K, dtype=torch.int16, device="cuda")
-    tvr_amd._lib.check(lib.tvr_split_planes_f16(W.data_ptr(), 2.0 ** 16, planes.data_ptr(), N * K, st), "split")
+    tvr_amd._lib.check(lib.tvr_weight_planes(X2F16, W.data_ptr(), 2.0 ** 16, planes.data_ptr(), N * K, st), "split")
     C = torch.empty(M, N, device="cuda")
     for big, want in ((4000.0, 0), (4100.0, 1)):
         A[5, 9] = big
@@ -164,7 +193,7 @@ def test_gemm_x2f16_range_flag():
         # the activation-format producers raise the same flag
         flag.zero_()
         Ah = torch.empty(M, 2, K, dtype=torch.int16, device="cuda")
-        tvr_amd._lib.check(lib.tvr_split_rows_f16(A.data_ptr(), K, Ah.data_ptr(), M, K, flag.data_ptr(), st), "rows")
+        tvr_amd._lib.check(lib.tvr_act_rows(X2F16, A.data_ptr(), K, Ah.data_ptr(), M, K, flag.data_ptr(), st), "rows")
         assert flag.item() == want, big
 
 
@@ -445,3 +474,48 @@ def test_x2f16_range_error_is_loud(tiny_cfg, tokenizer):
     m.set_gemm("x3bf16")
     out = m.forward_clean(prompts, targets=[1, 2])
     assert torch.isfinite(out["prob"]).all()
+
+
+# ------------------------------------------------------------------ bf16 mode
+# The north star's bf16 bar: extracted vectors within 2e-2 relative of the fp32
+# reference (only the GEMMs run in bf16; LayerNorm, attention, the residual
+# stream and softmax stay fp32).  Probabilities and CIE are bounded relative
+# to the largest probability involved.
+BF16_TOL = 2e-2
+
+
+@pytest.fixture(scope="module")
+def tiny_model_bf16(tiny_cfg, tiny_sd, tokenizer):
+    return tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer, gemm="bf16")
+
+
+def test_bf16_forward_and_extraction(tiny_model_bf16, tiny_oracle):
+    m = tiny_model_bf16
+    prompts = ragged_prompts(9, m.cfg.d_vocab, 1) + [[0], list(range(128))]
+    targets = [p[-1] for p in prompts]
+    out = m.forward_clean(prompts, targets=targets, return_logits=True)
+    for i, p in enumerate(prompts):
+        ref = tiny_oracle.forward(torch.tensor([p]))[0, -1]
+        assert rel_err(out["logits"][i], ref) < BF16_TOL, i
+        pr = torch.softmax(ref, 0)
+        assert abs(out["prob"][i].item() - pr[targets[i]].item()) <= BF16_TOL * pr.max().item()
+    random.seed(1234)
+    ours = tvr_amd.generate_mean_activation(tvr_amd.tasks.letter_to_caps, ARROW, ",", model=m,
+                                            num_contexts=96, len_contexts=4)
+    random.seed(1234)
+    ref = R.generate_mean_activation(tvr_amd.tasks.letter_to_caps, ARROW, ",", model=tiny_oracle,
+                                     num_contexts=96, len_contexts=4)
+    assert rel_err(ours, ref) < BF16_TOL
+
+
+def test_bf16_cie(tiny_model_bf16, tiny_oracle):
+    m = tiny_model_bf16
+    task = tvr_amd.tasks.letter_to_caps
+    random.seed(7)
+    mean = R.generate_mean_activation(task, ARROW, ",", model=tiny_oracle, num_contexts=32, len_contexts=4)
+    random.seed(8)
+    prompts, answers = tvr_amd.generate_shuffled_prompts(task, m, 3, 4, ARROW)
+    cie = tvr_amd.calculate_average_causal_indirect_effect(mean.cuda(), prompts, answers, model=m)
+    cie_ref = R.calculate_average_causal_indirect_effect(mean, prompts, answers, tiny_oracle)
+    pmax = max(torch.softmax(tiny_oracle.forward(m.to_tokens(p).cpu())[0, -1], 0).max().item() for p in prompts)
+    assert (cie.cpu().double() - cie_ref.double()).abs().max().item() <= BF16_TOL * pmax

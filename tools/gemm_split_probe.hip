@@ -2,10 +2,11 @@
 // paths (fp32 MFMA, 3-plane bf16 split, 2-plane fp16 split) at the engine's
 // real shapes, each checked against an fp64 reference on sampled rows.
 //   hipcc --offload-arch=gfx950 -O3 -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
-//   tools/gemm_split_probe [f32|x3|x2|x2p|x2pg|x2pt ...]   (default: f32 x3 x2 x2p)
+//   tools/gemm_split_probe [f32|x3|x2|x2p|x2pg|x2pt|bf16 ...]   (default: f32 x3 x2 x2p)
 //     x2p  = the engine's planar kernel (A pre-split, LDS-DMA, 16x16x32, EPI_BIAS)
 //     x2pg = the same with the QKV+MLP-in epilogue (bias, GELU, split-plane stores)
 //     x2pt = K-loop anatomy (cycles in vmcnt drain / barrier, waves 0 and 7)
+//     bf16 = the planar kernel on one bf16 plane (TVR_GEMM_BF16; its error is the bf16 rounding)
 // A is drawn N(0,1) (a LayerNorm output) or GELU(3 N(0,1)) (the MLP-out input:
 // many tiny values, which exercises the fp16 residual plane's range).
 #include <hip/hip_runtime.h>
@@ -17,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "../task-vector-replication_amd/csrc/gemm_planar.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x2f16.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x3bf16.hpp"
 
@@ -95,6 +97,11 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (const auto& path : paths) {
+      if (path == "bf16") {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
+        hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, dim3(8192), dim3(256), 0, 0, A, s.K, A2, s.M, s.K,
+                           (unsigned*)nullptr);  // [M][2][K] halves, plane 0 = bf16(A)
+        hipLaunchKernelGGL(bf16_plane_kernel, dim3(8192), dim3(256), 0, 0, W, W2, (size_t)s.N * s.K);
+      }
       GemmEpi e{}; e.out0 = C; e.ld0 = s.N;
       int grid = 0;
       auto run = [&](bool stamp) {
@@ -109,22 +116,27 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<EPI_BIAS, X3Large>), dim3(grid), dim3(X3Large::THREADS), 0, 0,
                              A, s.K, W3, s.K, (size_t)s.N * s.K, s.M, s.N, s.K, ee);
         } else if (path == "x2pt") {
-          grid = gemm_x2_grid<X2Large>(s.M, s.N);
-          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large, true, 2>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+          grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_X2F16, true, 2>), dim3(grid),
+                             dim3(PlanarLarge::THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2pg") {  // the engine's QKV+MLP-in epilogue: bias, GELU, split planes
-          grid = gemm_x2_grid<X2Large>(s.M, s.N);
+          grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
           GemmEpi eg = ee;
           eg.n_split = (s.N * 3 / 7) & ~3;  // ~3d of 3d + d_mlp
           eg.out1h = (uint16_t*)(C) + eg.n_split;  // reuse C: row stride 2N halves (bytes of the fp32 row)
           eg.ld1h = 2 * s.N;
           eg.ps1h = s.N;
           eg.range_flag = flag;
-          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_SPLIT_GELU_X2, X2Large, true, 0>), dim3(grid), dim3(X2Large::THREADS),
+          hipLaunchKernelGGL((gemm_planar_kernel<EPI_SPLIT_GELU_ACT, PlanarLarge, ACT_X2F16>), dim3(grid), dim3(PlanarLarge::THREADS),
                              0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+        } else if (path == "bf16") {  // bf16 planar: A2 / W2 re-filled with one bf16 plane below
+          grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_BF16>), dim3(grid), dim3(PlanarLarge::THREADS),
+                             0, 0, A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
         } else if (path == "x2p") {
-          grid = gemm_x2_grid<X2Large>(s.M, s.N);
-          hipLaunchKernelGGL((gemm_x2f16_planar_kernel<EPI_BIAS, X2Large>), dim3(grid), dim3(X2Large::THREADS), 0, 0,
+          grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_X2F16>), dim3(grid), dim3(PlanarLarge::THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else {
           grid = gemm_x2_grid<X2Large>(s.M, s.N);

@@ -36,14 +36,32 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16", "gemm_x2f16_planar_kernel": "x2f16"}
+FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16", "gemm_planar_kernel": "planar"}
+PLANAR_FMT = {"1": "x2f16", "2": "bf16"}  # gemm_planar_kernel<EPI, Tile, FMT, ...>
 
 
 def gemm_variant(name):
     """(family, epilogue variant) of a GEMM kernel name, or None."""
     for k, fam in FAMILIES.items():
         if k + "<" in name:
-            return fam, name.split(k + "<")[1][0]
+            args = name.split(k + "<")[1]
+            if fam == "planar":  # the third template argument is the activation format
+                depth, parts, cur = 0, [], ""
+                for ch in args:
+                    if ch == "<":
+                        depth += 1
+                    elif ch == ">":
+                        if depth == 0:
+                            break
+                        depth -= 1
+                    if ch == "," and depth == 0:
+                        parts.append(cur.strip())
+                        cur = ""
+                    else:
+                        cur += ch
+                parts.append(cur.strip())
+                fam = PLANAR_FMT.get(parts[2], "planar")
+            return fam, args[0]
     return None
 
 
