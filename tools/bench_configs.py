@@ -2,7 +2,8 @@
 """Measure the SURVEY.md §8(d) configurations on one GPU through the façade
 (the reference's own experiment functions), seeded synthetic weights.
 
-  python tools/bench_configs.py --configs C2,C3,C4 [--c4-tasks 2] > profiles/configs_rNN.json
+  python tools/bench_configs.py --configs C2,C3,C4 [--gemm x2f16] [--c4-gemm bf16] [--c4-tasks 20] \
+      > profiles/configs_rNN.json
 
 C2  Pythia-2.8B: extraction N=2048, 6-shot (T=28) on letter_to_caps; per-layer
     accuracy + Δprob sweeps over the 52 zero-shot prompts (1664 sites each).
@@ -36,9 +37,9 @@ def timed(fn):
     return out, time.perf_counter() - t
 
 
-def c2_c3(which):
+def c2_c3(which, gemm):
     res = {}
-    model = tvr_amd.Model.from_pretrained("pythia-2.8b", device="cuda")
+    model = tvr_amd.Model.from_pretrained("pythia-2.8b", device="cuda", gemm=gemm)
     task, arrow = tvr_amd.tasks.letter_to_caps, tvr_amd.tasks.ARROW
     random.seed(0)
     E.generate_mean_activation(task, arrow, model=model, num_contexts=64, len_contexts=6)  # warm
@@ -66,8 +67,8 @@ def c2_c3(which):
     return res
 
 
-def c4(n_tasks):
-    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device="cuda")
+def c4(n_tasks, gemm):
+    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device="cuda", gemm=gemm)
     arrow = tvr_amd.tasks.ARROW
     per_task = []
     for ti in range(n_tasks):
@@ -83,22 +84,26 @@ def c4(n_tasks):
         per_task.append({"task_seed": 100 + ti, "extraction_s": round(t_ex, 3), "cie_s": round(t_cie, 3),
                          "cie_patched_prompts_per_s": round(12 * 1024 / t_cie, 1), "fv_layer_sweep_s": round(t_fv, 3),
                          "total_s": round(time.perf_counter() - t0, 3), "fv_top5_acc_by_layer": acc})
-    return {"C4": {"dtype": "f32", "tasks": per_task,
+    cie_rate = sum(12 * 1024 / t["cie_s"] for t in per_task) / len(per_task)
+    return {"C4": {"gemm": gemm, "tasks": per_task, "mean_cie_patched_prompts_per_s": round(cie_rate, 1),
                    "mean_task_s": round(sum(t["total_s"] for t in per_task) / len(per_task), 3)}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C2,C3,C4")
-    ap.add_argument("--c4-tasks", type=int, default=2)
+    ap.add_argument("--gemm", default="x2f16", help="GEMM path of C2/C3 (fp32-accurate by default)")
+    ap.add_argument("--c4-gemm", default="bf16", help="GEMM path of C4 (BASELINE.json: bf16)")
+    ap.add_argument("--c4-tasks", type=int, default=20)
     a = ap.parse_args()
     which = set(a.configs.split(","))
-    out = {"gpu": torch.cuda.get_device_name(0), "weights": "seeded synthetic (no checkpoints offline)"}
+    out = {"gpu": torch.cuda.get_device_name(0), "weights": "seeded synthetic (no checkpoints offline)",
+           "gemm": a.gemm}
     if which & {"C2", "C3"}:
-        out.update(c2_c3(which))
+        out.update(c2_c3(which, a.gemm))
         torch.cuda.empty_cache()
     if "C4" in which:
-        out.update(c4(a.c4_tasks))
+        out.update(c4(a.c4_tasks, a.c4_gemm))
     print(json.dumps(out))
 
 
