@@ -1,0 +1,176 @@
+// attention_mfma.hpp — causal attention of short ragged sequences on the fp32
+// matrix cores: one wave per (sequence, head), no LDS, no block barriers.
+//
+// The patched forwards attend over T <= 128 positions (T = 15 at C3, 33 at
+// C5) with d_head <= 128.  Per (sequence, head) and 16-query tile:
+//   S^T = K Q^T    v_mfma_f32_16x16x4_f32, D[key][query]: lane l holds the
+//                  scores of query l&15 against keys 4(l>>4)+r, r = 0..3
+//   causal softmax per query (in-lane over r, then xor-16/32 shuffles)
+//   Z^T = V^T P^T  the S^T accumulator IS the B operand: in k step r lane
+//                  group g supplies key 4g + r, so V is read in that order;
+//                  D[dim][query]: lane l holds 4 consecutive dims of query
+//                  l&15 -> one 16-B store (fp32) / 8-B stores (activation
+//                  formats).
+// K, Q and V fragments are loaded from global memory straight into registers.
+// Lane group g owns dims [g DH/4, (g+1) DH/4) of Q and K (contiguous float4
+// loads); the rotary pairs (i, i + rd/2) with rd = DH/4 (every Pythia:
+// rotary_pct 0.25; the host checks it) stay inside lane group 0, at
+// compile-time register indices.  f32-input MFMA is exact fp32
+// (a k-ordered fmaf chain per step); the dot products are summed in a permuted
+// k order relative to a sequential loop, i.e. within fp32 rounding of
+// attention_kernel (kernels.hpp), whose TransformerLens semantics this keeps:
+// scores q.k / sqrt(d_head), -inf causal mask, fp32 softmax, z = P V.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+
+namespace tvr {
+
+constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
+
+// grid = ceil(n_seqs * n_heads / ATTM_WAVES) blocks of 64 * ATTM_WAVES threads;
+// NKT = key tiles the launch's longest sequence needs (1, 2, 4 or 8: the
+// register arrays are sized by it).  Latency-bound (short dependent MFMA
+// chains, global loads): as many waves per SIMD as the fragments allow without
+// spilling (4 at one key tile, 3 up to four, else 2).
+template <int FMT, int DH, int NKT>
+__global__ void __launch_bounds__(64 * ATTM_WAVES, (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4) ? 3 : 2)
+attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
+                      const SeqDesc* __restrict__ seqs, int n_seqs, int n_heads, void* __restrict__ z, int ldz,
+                      float* __restrict__ zf, int ldzf, unsigned* __restrict__ flag,
+                      const float* __restrict__ cos_t, const float* __restrict__ sin_t, int d,
+                      float inv_attn_scale) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int CH = DH / 4;    // dims per lane group in Q K^T
+  constexpr int NDT = DH / 16;  // 16-dim output tiles
+  constexpr int MAXKT = NKT;
+  static_assert(DH % 16 == 0 && DH <= 128 && NKT * 16 <= ATT_MAX_T, "d_head / key tiles");
+  const int lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
+  if (pair >= n_seqs * n_heads) return;  // a whole wave; nothing below synchronises
+  const int s = pair / n_heads, h = pair - s * n_heads;
+  const SeqDesc sd = seqs[s];
+  const int T = sd.p0 + sd.n;
+  const int nkt = (T + 15) >> 4;
+  const int li = lane & 15, g = lane >> 4;
+  constexpr int rd = CH, half = CH / 2;  // rotary_dim = d_head / 4
+
+  // row of absolute position j: the clean trace's prefix, or this run's rows
+  auto row_of = [&](int j) -> const float* {
+    return j < sd.p0 ? cache + (size_t)(sd.cache_row + j) * ldc : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
+  };
+  // dims [g CH, g CH + CH) of a Q or K head row, rotated for position pos
+  auto load_chunk = [&](const float* r, int pos, float (&x)[CH]) {
+#pragma unroll
+    for (int c = 0; c < CH; c += 4) {
+      const f4 v = *(const f4*)(r + g * CH + c);
+      x[c] = v[0];
+      x[c + 1] = v[1];
+      x[c + 2] = v[2];
+      x[c + 3] = v[3];
+    }
+    if (g == 0) {  // TL rotate-half rotary on dims [0, rd)
+#pragma unroll
+      for (int i = 0; i < half; ++i) {
+        const float x0 = x[i], x1 = x[i + half];
+        x[i] = x0 * cos_t[pos * rd + i] - x1 * sin_t[pos * rd + i];
+        x[i + half] = x1 * cos_t[pos * rd + i + half] + x0 * sin_t[pos * rd + i + half];
+      }
+    }
+  };
+
+  for (int q0 = sd.q0; q0 < sd.n; q0 += 16) {
+    // this lane's query column: relative row q0 + li (padding reuses the last row)
+    const int qi = min(q0 + li, sd.n - 1);
+    float qf[CH];
+    load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
+
+    f4 st[MAXKT];
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+      st[kt] = f4{0.f, 0.f, 0.f, 0.f};
+      if (kt < nkt) {
+        const int kj = min(16 * kt + li, T - 1);
+        float kf[CH];
+        load_chunk(row_of(kj) + d + h * DH, kj, kf);
+        // two accumulation chains (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
+        f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < CH; c += 2) {
+          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c], qf[c], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c + 1], qf[c + 1], a1, 0, 0, 0);
+        }
+        st[kt] = a0 + a1;
+      }
+      // one key tile's fragments live at a time (hoisting every tile's loads spills)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // causal softmax over keys 16kt + 4g + r for the query at absolute position qpos
+    const int qpos = sd.p0 + q0 + li;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * kt + 4 * g + r;
+        const float v = (kt < nkt && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
+        st[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - mx);
+        st[kt][r] = e;
+        sum += e;
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) st[kt][r] = st[kt][r] / sum;
+    }
+
+    f4 zt[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+      if (kt < nkt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+            zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (q0 + li < sd.n) {
+      const size_t zrow = (size_t)(sd.row0 + q0 + li);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int col = h * DH + 16 * dt + 4 * g;
+        const f4 v = zt[dt];
+        if constexpr (FMT != ACT_F32)
+          store_act4<FMT>((uint16_t*)z + zrow * 2 * ldz + col, ldz, v[0], v[1], v[2], v[3], flag);
+        else
+          *(f4*)((float*)z + zrow * ldz + col) = v;
+        if (zf) *(f4*)(zf + zrow * ldzf + col) = v;
+      }
+    }
+  }
+}
+
+}  // namespace tvr

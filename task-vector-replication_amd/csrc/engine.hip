@@ -13,12 +13,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "tvr.h"
 #include "gemm_f32.hpp"
+#include "attention_mfma.hpp"
 #include "gemm_planar.hpp"
 #include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
@@ -104,6 +106,7 @@ struct tvr_model {
   int gemm_mode = TVR_GEMM_F32;
   uint16_t* planes = nullptr;
   unsigned* range_flag = nullptr;  // device word: X2F16 input out of range since the last status read
+  bool att_mfma = true;            // attention_mfma_kernel where it applies (env TVR_ATTENTION=lds: the LDS kernel)
   std::vector<MatW> w1, w2;
   MatW wu;
   char* ws = nullptr;
@@ -327,14 +330,46 @@ struct Acts {
   int fmt;
 };
 
-// z: the z columns of a2 (fp32 or activation format fmt); zf: optional fp32 copy [rows][d]
+// z: the z columns of a2 (fp32 or activation format fmt); zf: optional fp32 copy [rows][d].
+// attention_mfma_kernel (one wave per (sequence, head), fp32 MFMA, no LDS)
+// for the Pythia head sizes (d_head 16 (tiny), 64, 80, 128) with
+// rotary_dim = d_head / 4 (every Pythia: rotary_pct 0.25), else attention_kernel.
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
                      int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
-  const size_t smem = attention_smem_bytes(maxT, c.d_head);
   const float inv_scale = 1.0f / std::sqrt((float)c.d_head);
+  const int dh = c.d_head;
+  if (m->att_mfma && c.rotary_dim == dh / 4 && (dh == 16 || dh == 64 || dh == 80 || dh == 128)) {
+    const int pairs = n_seqs * c.n_heads;
+    const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
+    const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : 8;
+#define TVR_ATTM(F, DHV, NK)                                                                                        \
+  hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
+                     n_seqs, c.n_heads, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d, inv_scale)
+#define TVR_ATTM_NK(F, DHV)                                                                     \
+  if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                            \
+  else if (nkt == 2) TVR_ATTM(F, DHV, 2);                                                       \
+  else if (nkt == 4) TVR_ATTM(F, DHV, 4);                                                       \
+  else TVR_ATTM(F, DHV, 8)
+#define TVR_ATTM_DH(F)                                                                          \
+  if (dh == 16) { TVR_ATTM_NK(F, 16); } else if (dh == 64) { TVR_ATTM_NK(F, 64); }              \
+  else if (dh == 80) { TVR_ATTM_NK(F, 80); } else { TVR_ATTM_NK(F, 128); }
+    if (fmt == ACT_X2F16) {
+      TVR_ATTM_DH(ACT_X2F16);
+    } else if (fmt == ACT_BF16) {
+      TVR_ATTM_DH(ACT_BF16);
+    } else {
+      TVR_ATTM_DH(ACT_F32);
+    }
+#undef TVR_ATTM_DH
+#undef TVR_ATTM_NK
+#undef TVR_ATTM
+    TVR_HIP(hipGetLastError());
+    return TVR_OK;
+  }
+  const size_t smem = attention_smem_bytes(maxT, c.d_head);
 #define TVR_ATT_LAUNCH(F)                                                                                     \
   do {                                                                                                        \
     if (smem > 64 * 1024)                                                                                     \
@@ -507,6 +542,7 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_laye
   m->layers.assign(layers, layers + cfg->n_layers);
   m->w_unembed_t = w_unembed_t;
   m->b_unembed = b_unembed;
+  if (const char* a = std::getenv("TVR_ATTENTION")) m->att_mfma = std::string(a) != "lds";
   for (int l = 0; l < cfg->n_layers; ++l) {
     m->w1.push_back(MatW{layers[l].w1});
     m->w2.push_back(MatW{layers[l].w2});
