@@ -519,3 +519,18 @@ def test_bf16_cie(tiny_model_bf16, tiny_oracle):
     cie_ref = R.calculate_average_causal_indirect_effect(mean, prompts, answers, tiny_oracle)
     pmax = max(torch.softmax(tiny_oracle.forward(m.to_tokens(p).cpu())[0, -1], 0).max().item() for p in prompts)
     assert (cie.cpu().double() - cie_ref.double()).abs().max().item() <= BF16_TOL * pmax
+
+
+def test_sweeps_are_deterministic(tiny_model):
+    """No atomics or unordered reductions on the result path: the same sweep
+    twice is bitwise identical (capture is a fixed-order two-pass sum)."""
+    task = tvr_amd.tasks.letter_to_caps
+    outs = []
+    for _ in range(2):
+        random.seed(11)
+        mean = tvr_amd.generate_mean_activation(task, ARROW, ",", model=tiny_model, num_contexts=40, len_contexts=4)
+        random.seed(12)
+        prompts, answers = tvr_amd.generate_shuffled_prompts(task, tiny_model, 3, 4, ARROW)
+        cie = tvr_amd.calculate_average_causal_indirect_effect(mean, prompts, answers, model=tiny_model)
+        outs.append((mean.cpu(), cie.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

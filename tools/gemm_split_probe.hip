@@ -134,6 +134,10 @@ int main(int argc, char** argv) {
           grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
           hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_BF16>), dim3(grid), dim3(PlanarLarge::THREADS),
                              0, 0, A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
+        } else if (path == "x2ps") {  // the 128x128 / 4-wave tile at the same shape (2 blocks per CU)
+          grid = gemm_planar_grid<PlanarSmall>(s.M, s.N);
+          hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarSmall, ACT_X2F16>), dim3(grid), dim3(PlanarSmall::THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2p") {
           grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
           hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_X2F16>), dim3(grid), dim3(PlanarLarge::THREADS), 0, 0,
