@@ -50,11 +50,12 @@ PEAKS = {"f32": FP32_MFMA_PEAK_TFLOPS, **{k: BF16_MFMA_PEAK_TFLOPS / v for k, v 
 KERNELS = {"f32": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused epilogues)",
            "x3bf16": "gemm_x3bf16_nt_kernel (3-plane bf16 split on v_mfma_f32_32x32x16_bf16, 6 products, "
                      "fp32 accumulate; all three fused epilogues)",
-           "x2f16": "gemm_planar_kernel<ACT_X2F16> (2-plane fp16 split activations written by their producers, "
-                    "LDS-DMA staging, 3 products on v_mfma_f32_16x16x32_f16, fp32 accumulate; all three fused "
-                    "epilogues)",
-           "bf16": "gemm_planar_kernel<ACT_BF16> (bf16 weights and activations, LDS-DMA staging, "
-                   "v_mfma_f32_16x16x32_bf16, fp32 accumulate; all three fused epilogues)"}
+           "x2f16": "gemm_pingpong_kernel<ACT_X2F16> (2-plane fp16 split activations written by their producers, "
+                    "LDS-DMA staging with counted waits, 4 phases per k-tile, two wave groups one barrier apart, "
+                    "3 products on v_mfma_f32_16x16x32_f16, fp32 accumulate; all three fused epilogues)",
+           "bf16": "gemm_pingpong_kernel<ACT_BF16> (bf16 weights and activations, LDS-DMA staging with counted "
+                   "waits, two wave groups one barrier apart, v_mfma_f32_16x16x32_bf16, fp32 accumulate; all "
+                   "three fused epilogues)"}
 
 
 def parse():

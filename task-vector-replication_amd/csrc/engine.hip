@@ -21,6 +21,7 @@
 #include "tvr.h"
 #include "gemm_f32.hpp"
 #include "attention_mfma.hpp"
+#include "gemm_pingpong.hpp"
 #include "gemm_planar.hpp"
 #include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
@@ -211,6 +212,16 @@ hipEvent_t prof_event(tvr_model* m) {
   return e;
 }
 
+// Large planar launches run gemm_pingpong_kernel; TVR_GEMM_SCHED=planar selects
+// the one-barrier gemm_planar_kernel instead (A/B runs).
+bool gemm_pingpong_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TVR_GEMM_SCHED");
+    return !(e && std::string(e) == "planar");
+  }();
+  return on;
+}
+
 // Activation format of the model's GEMM inputs (split.hpp).
 int act_fmt(const tvr_model* m) {
   return m->gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : m->gemm_mode == TVR_GEMM_BF16 ? ACT_BF16 : ACT_F32;
@@ -251,16 +262,26 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   const float* Af = static_cast<const float*>(A);
   const uint16_t* Ah = static_cast<const uint16_t*>(A);
   const bool vec = planar_epilogue_vec(epi, ep, N);
+  const bool pingpong = gemm_pingpong_enabled();
 #define TVR_PL_LAUNCH2(E, TL, F, V)                                                                         \
   hipLaunchKernelGGL((gemm_planar_kernel<E, TL, F, V>), dim3(gemm_planar_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
 #define TVR_PL_LAUNCH1(E, TL, F) \
   if (vec) TVR_PL_LAUNCH2(E, TL, F, true); else TVR_PL_LAUNCH2(E, TL, F, false)
+#define TVR_PP_LAUNCH2(E, F, V)                                                                              \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), dim3(gemm_pingpong_grid(M, N)), dim3(PP_THREADS), 0, st, \
+                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_PL_LARGE(E, F)                                                   \
+  if (pingpong) {                                                            \
+    if (vec) TVR_PP_LAUNCH2(E, F, true); else TVR_PP_LAUNCH2(E, F, false);  \
+  } else {                                                                   \
+    TVR_PL_LAUNCH1(E, PlanarLarge, F);                                       \
+  }
 #define TVR_PL_LAUNCH(E)                                                                               \
   if (a_fmt == ACT_X2F16) {                                                                              \
-    if (large) { TVR_PL_LAUNCH1(E, PlanarLarge, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
+    if (large) { TVR_PL_LARGE(E, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
   } else {                                                                                               \
-    if (large) { TVR_PL_LAUNCH1(E, PlanarLarge, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
+    if (large) { TVR_PL_LARGE(E, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
   }
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
@@ -286,6 +307,8 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
 #undef TVR_X3_LAUNCH
 #undef TVR_X2_LAUNCH
 #undef TVR_PL_LAUNCH
+#undef TVR_PL_LARGE
+#undef TVR_PP_LAUNCH2
 #undef TVR_PL_LAUNCH1
 #undef TVR_PL_LAUNCH2
 #undef TVR_GEMM_LAUNCH

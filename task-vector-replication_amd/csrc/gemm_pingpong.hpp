@@ -1,0 +1,236 @@
+// gemm_pingpong.hpp — the planar GEMM (gemm_planar.hpp: same operands, same
+// LDS image, same fused epilogues) on a phase-split, two-group schedule.
+//
+//   C[M][N] = A[M][K] @ W[N][K]^T (+ fused epilogue), A and W in a planar
+//   activation format (ACT_X2F16: 2 fp16 planes, BK 32; ACT_BF16: 1 bf16
+//   plane, BK 64) — 128 B of K per row per k-tile in both.
+//
+// Block 256 x 256, 8 waves as 2 (rows, wr) x 4 (columns, wc), 128 x 64 output
+// per wave (8 x 4 accumulators of 16 x 16, D = W A^T as in gemm_planar.hpp).
+// Why a new schedule: in gemm_planar_kernel both waves of a SIMD read LDS and
+// issue MFMAs at the same time and meet at one barrier per k-tile; the older
+// wave wins issue, finishes first and waits at the barrier 36 % of its loop
+// (profiles/gemm_x2_variants_r01.json) — the SIMD's MFMA pipe is 55 % busy.
+// Here each k-tile is 4 phases, one output quadrant each:
+//     q1  Q(A_lo, W_lo)   reads A_lo (8 fragments) + W_lo (4)
+//     q2  Q(A_lo, W_hi)   reads W_hi (4)
+//     q3  Q(A_hi, W_hi)   reads A_hi (8)
+//     q4  Q(A_hi, W_lo)   no reads (W_lo still in registers)
+// and every phase is  [ds_reads, LDS-DMA issue] barrier [MFMA cluster] barrier.
+// Waves 4-7 (wr = 1) pass one extra barrier before the loop, so on every SIMD
+// one wave runs its MFMA cluster while its partner reads LDS and issues its
+// loads: the MFMA pipe always has a wave to feed it.
+//
+// Staging (LDS-DMA, 2 buffers): a k-tile is 4 regions of 16 KB (A_lo = rows
+// 0-63 of each wave-row's 128, A_hi, W_lo = columns 0-31 of each wave-column's
+// 64, W_hi), each 16 x 1 KB pieces, 2 per wave.  A region is restaged for the
+// tile two ahead (same buffer) two phases after its last read — q1 stages
+// A_hi(t+1), q3 A_lo(t+2) and W_lo(t+2), q4 W_hi(t+2) — which is the WAR
+// margin the one-barrier group offset needs (a wave of the other group may
+// still be reading one segment later).  Every region lands >= 6 phases after it
+// is issued and is retired one phase before its first read by a COUNTED wait:
+// vmcnt(8) before the stage of q1, q2 and q4 (8 = the glds issued since), then
+// the phase's barrier; nothing in the loop waits vmcnt(0) and no
+// __syncthreads() (its fence would drain the DMA).  Past the last k-tile the
+// stage still issues (same counts) into a 1 KB LDS region nobody reads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gemm_planar.hpp"
+
+namespace tvr {
+
+constexpr int PP_THREADS = 512;
+
+inline int gemm_pingpong_grid(int M, int N) { return ((M + 255) / 256) * ((N + 255) / 256); }
+
+// K must be a multiple of BK (host-checked); any M, N.
+// VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
+// (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
+// waits in the loop (racy: timing only).
+template <int EPI, int FMT, bool VEC = true, int VAR = 0>
+__global__ void __launch_bounds__(PP_THREADS, 1)
+gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
+                     size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
+  using F = PlanarFmt<FMT>;
+  using frag = typename F::frag;
+  const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;  // clock diagnostics
+  const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  constexpr int NPL = F::NPL, BK = F::BK, KG = BK / 32;
+  constexpr int CPR = BK / 8;          // 16-B chunks per plane row
+  constexpr int RPP = 64 / CPR;        // rows per 1 KB piece
+  constexpr int PPP = 128 / RPP;       // pieces per plane per region (128 rows)
+  constexpr int PL = 256 * BK;         // halves per plane per buffer
+  constexpr int BUF = 2 * NPL * PL;    // halves per buffer: A planes, then W planes
+  constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
+  static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
+  static_assert((2 * BUF + 512) * 2 <= 160 * 1024, "LDS budget");
+  // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF + 512];
+
+  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8, nwg = nbm * nbn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GEMM_GROUP_M * nbn;
+  const int grp = wg / per_group;
+  const int first_m = grp * GEMM_GROUP_M;
+  const int gsz = min(nbm - first_m, GEMM_GROUP_M);
+  const int in_grp = wg - grp * per_group;
+  const int m0 = (first_m + in_grp % gsz) * 256, n0 = (in_grp / gsz) * 256;
+
+  const int t = threadIdx.x;
+  const int wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- staging map: region R (0 A_lo, 1 A_hi, 2 W_lo, 3 W_hi), pieces 2 wave + s
+  const uint16_t* src[4][2];
+  int dst[4][2];
+#pragma unroll
+  for (int R = 0; R < 4; ++R) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int pi = 2 * wave + s;
+      const int plane = pi / PPP, x0 = (pi % PPP) * RPP;  // region row of the piece's first row
+      int trow0;                                          // tile row of it
+      if (R < 2)
+        trow0 = ((x0 >> 6) << 7) + (x0 & 63) + 64 * R;
+      else
+        trow0 = ((x0 >> 5) << 6) + (x0 & 31) + 32 * (R - 2);
+      const int row = trow0 + lane / CPR;
+      const int chunk = (lane % CPR) ^ planar_g<CPR>(row);
+      if (R < 2) {
+        const int am = min(m0 + row, M - 1);
+        src[R][s] = A + plane * aps + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + chunk * 8;
+        dst[R][s] = plane * PL + trow0 * BK;
+      } else {
+        src[R][s] = W + plane * wps + (size_t)min(n0 + row, N - 1) * ldw + chunk * 8;
+        dst[R][s] = (NPL + plane) * PL + trow0 * BK;
+      }
+    }
+  }
+  const int nk = K / BK;
+  auto stage = [&](int R, int kt) {
+    if (VAR == 1 && kt >= 2) return;
+    const bool live = kt < nk;
+    const int koff = live ? kt * BK : 0;
+    const int boff = (kt & 1) * BUF;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
+  };
+
+  // ---- fragment offsets (halves, within a buffer); f = plane (x2f16) or k group (bf16)
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int p = NPL == 2 ? f : 0, g = NPL == 2 ? 0 : f;
+    const int ra = wr * 128 + (lane & 15), rb = wc * 64 + (lane & 15);
+    const int c = 4 * g + (lane >> 4);
+    aoff[f] = p * PL + ra * BK + ((c ^ planar_g<CPR>(ra)) << 3);
+    boff[f] = (NPL + p) * PL + rb * BK + ((c ^ planar_g<CPR>(rb)) << 3);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+  frag fa[4][2], fwl[2][2], fwh[2][2];
+
+  auto read_a = [&](const uint16_t* base, int i0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) fa[i][f] = *(const frag*)(base + aoff[f] + (i0 + i) * 16 * BK);
+  };
+  auto read_w = [&](const uint16_t* base, int j0, frag (&fw)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
+  };
+  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4 c = acc[i0 + i][j0 + j];
+        if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][0], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][1], fa[i][1], c, 0, 0, 0);
+        }
+        acc[i0 + i][j0 + j] = c;
+      }
+  };
+  // [MFMA cluster] between this phase's two barriers
+#define TVR_PP_CLUSTER(...)                  \
+  __builtin_amdgcn_s_barrier();              \
+  __builtin_amdgcn_sched_barrier(0);         \
+  if (VAR != 2) __builtin_amdgcn_s_setprio(1); \
+  __VA_ARGS__;                               \
+  if (VAR != 2) __builtin_amdgcn_s_setprio(0); \
+  __builtin_amdgcn_sched_barrier(0);         \
+  __builtin_amdgcn_s_barrier();              \
+  __builtin_amdgcn_sched_barrier(0)
+
+  // ---- prologue: the stage history of tiles -2 and -1, then retire A_lo(0) / W_lo(0)
+  stage(0, 0);
+  stage(2, 0);
+  stage(3, 0);
+  stage(1, 0);
+  stage(0, 1);
+  stage(2, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  stage(3, 1);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (wr == 1 && VAR != 3) {  // the group offset: waves 4-7 run one barrier behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* cur = lds + (kt & 1) * BUF;
+    // q1: Q(A_lo, W_lo)
+    read_a(cur, 0);
+    read_w(cur, 0, fwl);
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // W_hi(kt), read in q2
+    stage(1, kt + 1);
+    TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl));
+    // q2: Q(A_lo, W_hi)
+    read_w(cur, 2, fwh);
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt), read in q3
+    TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh));
+    // q3: Q(A_hi, W_hi)
+    read_a(cur, 4);
+    stage(0, kt + 2);
+    stage(2, kt + 2);
+    TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh));
+    // q4: Q(A_hi, W_lo)
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1), read in q1
+    stage(3, kt + 2);
+    TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl));
+  }
+#undef TVR_PP_CLUSTER
+  if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sink's DMAs retire before the block ends
+
+  if (acc_scale != 1.0f) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
+  }
+  gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+  if (ep.stamps && t == 0) {
+    ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
+    ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+  }
+}
+
+}  // namespace tvr

@@ -7,6 +7,7 @@
 //     x2pg = the same with the QKV+MLP-in epilogue (bias, GELU, split-plane stores)
 //     x2pt = K-loop anatomy (cycles in vmcnt drain / barrier, waves 0 and 7)
 //     bf16 = the planar kernel on one bf16 plane (TVR_GEMM_BF16; its error is the bf16 rounding)
+//     x2pp / bf16pp = the phase-split two-group schedule (gemm_pingpong.hpp); bf16 paths last
 // A is drawn N(0,1) (a LayerNorm output) or GELU(3 N(0,1)) (the MLP-out input:
 // many tiny values, which exercises the fp16 residual plane's range).
 #include <hip/hip_runtime.h>
@@ -18,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "../task-vector-replication_amd/csrc/gemm_pingpong.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_planar.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x2f16.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x3bf16.hpp"
@@ -97,7 +99,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (const auto& path : paths) {
-      if (path == "bf16") {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
+      if (path == "bf16" || path == "bf16pp") {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
         hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, dim3(8192), dim3(256), 0, 0, A, s.K, A2, s.M, s.K,
                            (unsigned*)nullptr);  // [M][2][K] halves, plane 0 = bf16(A)
         hipLaunchKernelGGL(bf16_plane_kernel, dim3(8192), dim3(256), 0, 0, W, W2, (size_t)s.N * s.K);
@@ -134,6 +136,22 @@ int main(int argc, char** argv) {
           grid = gemm_planar_grid<PlanarLarge>(s.M, s.N);
           hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarLarge, ACT_BF16>), dim3(grid), dim3(PlanarLarge::THREADS),
                              0, 0, A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
+        } else if (path == "x2pp") {  // phase-split two-group schedule (gemm_pingpong.hpp)
+          grid = gemm_pingpong_grid(s.M, s.N);
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4") {  // diagnostic variants
+          grid = gemm_pingpong_grid(s.M, s.N);
+          auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
+                    : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
+                    : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
+                                      : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
+          hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "bf16pp") {
+          grid = gemm_pingpong_grid(s.M, s.N);
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
         } else if (path == "x2ps") {  // the 128x128 / 4-wave tile at the same shape (2 blocks per CU)
           grid = gemm_planar_grid<PlanarSmall>(s.M, s.N);
           hipLaunchKernelGGL((gemm_planar_kernel<EPI_BIAS, PlanarSmall, ACT_X2F16>), dim3(grid), dim3(PlanarSmall::THREADS), 0, 0,
