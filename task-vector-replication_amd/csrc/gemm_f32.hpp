@@ -73,9 +73,29 @@ struct GemmEpi {
   unsigned long long* stamps;
 };
 
+// torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":
+// x Phi(x), Phi from erfc(|x| / sqrt 2) = t exp(-z^2 + P(t)), t = 1 / (1 + z/2),
+// P the degree-9 Chebyshev fit of Press et al. (Numerical Recipes, erfcc;
+// relative error < 1.2e-7 on erfc everywhere).  Branch-free (the GEMM
+// epilogue applies it to every lane: ocml erff diverges into two paths, 3x the
+// instructions); |error| <= 1.2e-7 max(1, |x|), as 0.5 x (1 + erff(x / sqrt 2))
+// in fp32, and relative accuracy holds on the negative tail (no 1 + erf
+// cancellation).
 __device__ __forceinline__ float gelu_erf(float x) {
-  // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu"
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float h = 0.5f * t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.44269504088896341f);  // erfc(z) / 2
+  return x * (x >= 0.0f ? 1.0f - h : h);
 }
 
 // One output element of the fused epilogues (v = acc + bias already); FMT is

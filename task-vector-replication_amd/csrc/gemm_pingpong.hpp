@@ -48,7 +48,9 @@ inline int gemm_pingpong_grid(int M, int N) { return ((M + 255) / 256) * ((N + 2
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
 // (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
-// waits in the loop (racy: timing only).
+// waits in the loop (racy: timing only), 5 LDS-DMA issued inside the MFMA
+// clusters instead of the read segments, 6 per-block stamps (start, loop
+// start, loop end, end) of wave 0 to ep.stamps[4 block + i].
 template <int EPI, int FMT, bool VEC = true, int VAR = 0>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
@@ -150,9 +152,9 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
 #pragma unroll
       for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
   };
-  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2]) {
+  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], int ib = 0, int ie = 4) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = ib; i < ie; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x4 c = acc[i0 + i][j0 + j];
@@ -177,6 +179,11 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   __builtin_amdgcn_sched_barrier(0);         \
   __builtin_amdgcn_s_barrier();              \
   __builtin_amdgcn_sched_barrier(0)
+  // an MFMA cluster with LDS-DMA issues pinned between its parts
+#define TVR_PP_PIN(...)              \
+  __builtin_amdgcn_sched_barrier(0); \
+  __VA_ARGS__;                       \
+  __builtin_amdgcn_sched_barrier(0)
 
   // ---- prologue: the stage history of tiles -2 and -1, then retire A_lo(0) / W_lo(0)
   stage(0, 0);
@@ -194,8 +201,25 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  unsigned long long d_loop0 = 0, d_loop1 = 0;
+  if constexpr (VAR == 6) d_loop0 = __builtin_amdgcn_s_memtime();
   for (int kt = 0; kt < nk; ++kt) {
     const uint16_t* cur = lds + (kt & 1) * BUF;
+    if constexpr (VAR == 5) {  // LDS-DMA issued inside the MFMA clusters (same order, same counts)
+      read_a(cur, 0);
+      read_w(cur, 0, fwl);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, 0, 2); TVR_PP_PIN(stage(1, kt + 1)); mfma_quadrant(0, 0, fwl, 2, 4));
+      read_w(cur, 2, fwh);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh));
+      read_a(cur, 4);
+      TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, 0, 1); TVR_PP_PIN(stage(0, kt + 2)); mfma_quadrant(4, 2, fwh, 1, 2);
+                     TVR_PP_PIN(stage(2, kt + 2)); mfma_quadrant(4, 2, fwh, 2, 4));
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, 0, 2); TVR_PP_PIN(stage(3, kt + 2)); mfma_quadrant(4, 0, fwl, 2, 4));
+      continue;
+    }
     // q1: Q(A_lo, W_lo)
     read_a(cur, 0);
     read_w(cur, 0, fwl);
@@ -217,6 +241,8 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl));
   }
 #undef TVR_PP_CLUSTER
+#undef TVR_PP_PIN
+  if constexpr (VAR == 6) d_loop1 = __builtin_amdgcn_s_memtime();
   if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sink's DMAs retire before the block ends
 
@@ -227,7 +253,13 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
   }
   gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
-  if (ep.stamps && t == 0) {
+  if (VAR == 6 && ep.stamps && t == 0) {
+    unsigned long long* o = ep.stamps + 4 * blockIdx.x;
+    o[0] = st0;
+    o[1] = d_loop0;
+    o[2] = d_loop1;
+    o[3] = __builtin_amdgcn_s_memtime();
+  } else if (ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
   }

@@ -68,7 +68,7 @@ int main(int argc, char** argv) {
     hipMalloc(&C, sizeof(float) * (size_t)s.M * s.N);
     hipMalloc(&flag, 8);
     hipMalloc(&wmax_bits, 8);
-    hipMalloc(&stamps, sizeof(unsigned long long) * 6 * maxgrid);
+    hipMalloc(&stamps, sizeof(unsigned long long) * 6 * (size_t)maxgrid);
     hipMemset(flag, 0, 8);
     hipMemset(wmax_bits, 0, 8);
     hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, A, (size_t)s.M * s.K, 11u, s.gelu ? 3.0f : 1.0f, s.gelu);
@@ -140,14 +140,40 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4") {  // diagnostic variants
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp5") {  // diagnostic variants
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
                     : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
                     : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
+                    : path == "x2pp5" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 5>
                                       : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
           hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2ppg") {  // pingpong with the QKV+MLP-in epilogue, timed
+          grid = gemm_pingpong_grid(s.M, s.N);
+          GemmEpi eg = ee;
+          eg.n_split = (s.N * 3 / 7) & ~3;
+          eg.out1h = (uint16_t*)(C) + eg.n_split;
+          eg.ld1h = 2 * s.N;
+          eg.ps1h = s.N;
+          eg.range_flag = flag;
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 0>), dim3(grid), dim3(PP_THREADS),
+                             0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+        } else if (path == "x2pp6" || path == "x2pp6g") {  // per-block anatomy (prologue / loop / epilogue)
+          grid = gemm_pingpong_grid(s.M, s.N);
+          GemmEpi eg = ee;
+          if (path == "x2pp6g") {
+            eg.n_split = (s.N * 3 / 7) & ~3;
+            eg.out1h = (uint16_t*)(C) + eg.n_split;
+            eg.ld1h = 2 * s.N;
+            eg.ps1h = s.N;
+            eg.range_flag = flag;
+            hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 6>), dim3(grid), dim3(PP_THREADS),
+                               0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+          } else {
+            hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 6>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                               A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+          }
         } else if (path == "bf16pp") {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16>), dim3(grid), dim3(PP_THREADS), 0, 0,
@@ -166,6 +192,26 @@ int main(int argc, char** argv) {
                              A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
         }
       };
+      if (path == "x2pp6" || path == "x2pp6g") {  // block anatomy: medians over blocks (cycles)
+        for (int i = 0; i < 5; ++i) run(false);
+        run(true);
+        hipDeviceSynchronize();
+        std::vector<unsigned long long> hs(4 * (size_t)grid);
+        hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost);
+        std::vector<double> pro, loop, epi;
+        for (int g = 0; g < grid; ++g) {
+          pro.push_back((double)(hs[4 * g + 1] - hs[4 * g]));
+          loop.push_back((double)(hs[4 * g + 2] - hs[4 * g + 1]));
+          epi.push_back((double)(hs[4 * g + 3] - hs[4 * g + 2]));
+        }
+        std::sort(pro.begin(), pro.end()); std::sort(loop.begin(), loop.end()); std::sort(epi.begin(), epi.end());
+        printf("{\"shape\": \"%s\", \"path\": \"%s\", \"prologue_cyc\": %.0f, \"loop_cyc\": %.0f, "
+               "\"loop_cyc_per_ktile\": %.1f, \"epilogue_cyc\": %.0f, \"epilogue_p90\": %.0f}\n", s.name, path.c_str(),
+               pro[pro.size() / 2], loop[loop.size() / 2], loop[loop.size() / 2] / (s.K / 32), epi[epi.size() / 2],
+               epi[epi.size() * 9 / 10]);
+        fflush(stdout);
+        continue;
+      }
       if (path == "x2pt") {  // K-loop anatomy: waves 0 and 7, medians over blocks
         run(true);
         hipDeviceSynchronize();
