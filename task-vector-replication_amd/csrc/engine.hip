@@ -112,6 +112,8 @@ struct tvr_model {
   MatW wu;
   char* ws = nullptr;
   size_t ws_bytes = 0;
+  float* splitk_ws = nullptr;  // split-K partial products (launch_gemm), grown on demand
+  size_t splitk_bytes = 0;
   Staging staging;
   // profiling (tvr_profile_enable): event pairs around GEMM launches
   bool prof = false;
@@ -147,6 +149,22 @@ int ensure_workspace(tvr_model* m, size_t bytes, hipStream_t st) {
     return fail(TVR_ERR_NOMEM, "workspace allocation of " + std::to_string(want) + " bytes failed");
   }
   m->ws_bytes = want;
+  return TVR_OK;
+}
+
+int ensure_splitk(tvr_model* m, size_t bytes, hipStream_t st) {
+  if (bytes <= m->splitk_bytes) return TVR_OK;
+  TVR_HIP(hipStreamSynchronize(st));
+  if (m->splitk_ws) TVR_HIP(hipFree(m->splitk_ws));
+  m->splitk_ws = nullptr;
+  m->splitk_bytes = 0;
+  const size_t want = align_up(bytes);
+  if (hipMalloc(&m->splitk_ws, want) != hipSuccess) {
+    m->splitk_ws = nullptr;
+    (void)hipGetLastError();
+    return fail(TVR_ERR_NOMEM, "split-K workspace allocation of " + std::to_string(want) + " bytes failed");
+  }
+  m->splitk_bytes = want;
   return TVR_OK;
 }
 
@@ -212,13 +230,30 @@ hipEvent_t prof_event(tvr_model* m) {
   return e;
 }
 
-// Large planar launches run gemm_pingpong_kernel; TVR_GEMM_SCHED=planar selects
-// the one-barrier gemm_planar_kernel instead (A/B runs).
+// Planar launches run gemm_pingpong_kernel (split-K below 192 tiles; measured
+// faster than the 128x128 tile at every size the sweeps produce);
+// TVR_GEMM_SCHED=planar selects gemm_planar_kernel (256x256 from 512 tiles,
+// else 128x128) instead, for A/B runs.
 bool gemm_pingpong_enabled() {
   static const bool on = [] {
     const char* e = getenv("TVR_GEMM_SCHED");
     return !(e && std::string(e) == "planar");
   }();
+  return on;
+}
+// A/B knobs of the planar launch policy (default both on): TVR_GEMM_SPLITK=0
+// disables split-K, TVR_GEMM_PP_SMALL=0 sends launches below 512 tiles to the
+// 128x128 gemm_planar_kernel instead of gemm_pingpong_kernel.
+bool env_flag(const char* name) {
+  const char* e = getenv(name);
+  return !(e && std::string(e) == "0");
+}
+bool gemm_splitk_enabled() {
+  static const bool on = env_flag("TVR_GEMM_SPLITK");
+  return on;
+}
+bool gemm_pp_small_enabled() {
+  static const bool on = env_flag("TVR_GEMM_PP_SMALL");
   return on;
 }
 
@@ -262,7 +297,7 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   const float* Af = static_cast<const float*>(A);
   const uint16_t* Ah = static_cast<const uint16_t*>(A);
   const bool vec = planar_epilogue_vec(epi, ep, N);
-  const bool pingpong = gemm_pingpong_enabled();
+  const bool pingpong = gemm_pingpong_enabled(), pp_small = gemm_pp_small_enabled();
 #define TVR_PL_LAUNCH2(E, TL, F, V)                                                                         \
   hipLaunchKernelGGL((gemm_planar_kernel<E, TL, F, V>), dim3(gemm_planar_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
@@ -279,9 +314,9 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   }
 #define TVR_PL_LAUNCH(E)                                                                               \
   if (a_fmt == ACT_X2F16) {                                                                              \
-    if (large) { TVR_PL_LARGE(E, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
+    if (large || (pingpong && pp_small)) { TVR_PL_LARGE(E, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
   } else {                                                                                               \
-    if (large) { TVR_PL_LARGE(E, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
+    if (large || (pingpong && pp_small)) { TVR_PL_LARGE(E, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
   }
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
@@ -296,6 +331,43 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   }
 #define TVR_GEMM_PICK(E) \
   if (planar) { TVR_PL_LAUNCH(E); } else { TVR_GEMM_PICK_NP(E); }
+  // Split-K: a planar launch of fewer than 192 256x256 tiles (the clean
+  // forward's 180-row GEMMs, layer sweeps) cannot fill 256 CUs; its K range is
+  // split so tiles x splits fills them, each split writes an fp32 partial
+  // product and splitk_reduce_kernel sums the splits in order and applies the
+  // epilogue (deterministic; a different summation order than one block).
+  int ksplit = 1;
+  if (planar && pingpong && m && vec && gemm_splitk_enabled()) {
+    const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_BF16 ? 64 : 32);
+    if (tiles < 192) ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
+  }
+  if (ksplit > 1) {
+    const int rc = ensure_splitk(m, (size_t)ksplit * M * N * sizeof(float), st);
+    if (rc != TVR_OK) return rc;
+    GemmEpi pe{};
+    pe.out0 = m->splitk_ws;
+    pe.ld0 = N;
+    pe.a_rows = ep.a_rows;
+    pe.k_split = ksplit;
+    const dim3 g(gemm_pingpong_grid(M, N) * ksplit), rg(std::min(2048, (M * (N / 4) + 255) / 256));
+    if (a_fmt == ACT_X2F16)
+      hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                         (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+    else
+      hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                         (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+#define TVR_SK_REDUCE(E, F) \
+  hipLaunchKernelGGL((splitk_reduce_kernel<E, F>), rg, dim3(256), 0, st, (const float*)m->splitk_ws, ksplit, M, N, ep)
+#define TVR_SK_REDUCE_F(E) \
+  if (a_fmt == ACT_X2F16) { TVR_SK_REDUCE(E, ACT_X2F16); } else { TVR_SK_REDUCE(E, ACT_BF16); }
+    switch (epi) {
+      case EPI_BIAS: TVR_SK_REDUCE_F(EPI_BIAS); break;
+      case EPI_SPLIT_GELU_ACT: TVR_SK_REDUCE_F(EPI_SPLIT_GELU_ACT); break;
+      default: TVR_SK_REDUCE_F(EPI_RESID); break;
+    }
+#undef TVR_SK_REDUCE_F
+#undef TVR_SK_REDUCE
+  } else
   switch (epi) {
     case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
     case EPI_SPLIT_GELU: TVR_GEMM_PICK_NP(EPI_SPLIT_GELU); break;
@@ -611,6 +683,7 @@ int tvr_model_destroy(tvr_model* m) {
   if (m->planes) (void)hipFree(m->planes);
   if (m->range_flag) (void)hipFree(m->range_flag);
   if (m->ws) (void)hipFree(m->ws);
+  if (m->splitk_ws) (void)hipFree(m->splitk_ws);
   for (auto& r : m->prof_recs) {
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);

@@ -71,6 +71,11 @@ struct GemmEpi {
   // Diagnostics only (tools/gemm_probe.hip; the engine passes nullptr): per
   // block {Δs_memtime, Δs_memrealtime} to read the shader clock under load.
   unsigned long long* stamps;
+  // gemm_pingpong_kernel split-K (engine: small-M launches): > 1 runs
+  // tiles x k_split blocks, each writing its fp32 partial product to
+  // out0 + split * M * ld0 (EPI_BIAS, bias nullptr); splitk_reduce_kernel sums
+  // the splits in order and applies the real epilogue.
+  int k_split;
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":

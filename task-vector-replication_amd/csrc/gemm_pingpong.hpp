@@ -71,10 +71,13 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF + 512];
 
-  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8, nwg = nbm * nbn;
+  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
+  const int S = ep.k_split > 1 ? ep.k_split : 1;  // split-K: block = (tile, split)
+  const int nwg = nbm * nbn * S;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int wgs = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int wg = wgs / S, split = wgs - wg * S;
   const int per_group = GEMM_GROUP_M * nbn;
   const int grp = wg / per_group;
   const int first_m = grp * GEMM_GROUP_M;
@@ -112,11 +115,13 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       }
     }
   }
-  const int nk = K / BK;
+  const int nk_all = K / BK;
+  const int kbeg = (int)((long long)split * nk_all / S);
+  const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
   auto stage = [&](int R, int kt) {
     if (VAR == 1 && kt >= 2) return;
     const bool live = kt < nk;
-    const int koff = live ? kt * BK : 0;
+    const int koff = live ? (kbeg + kt) * BK : 0;
     const int boff = (kt & 1) * BUF;
 #pragma unroll
     for (int s = 0; s < 2; ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
@@ -252,7 +257,13 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
   }
-  gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+  if (S > 1) {  // partial product of this split (EPI_BIAS launches only; host-checked)
+    GemmEpi pe = ep;
+    pe.out0 = ep.out0 + (size_t)split * M * ep.ld0;
+    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+  } else {
+    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+  }
   if (VAR == 6 && ep.stamps && t == 0) {
     unsigned long long* o = ep.stamps + 4 * blockIdx.x;
     o[0] = st0;
@@ -262,6 +273,27 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   } else if (ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+  }
+}
+
+// Sum of the k_split partial products [S][M][N] (fixed order: deterministic)
+// + bias, then the launch's real epilogue on four consecutive columns per
+// thread (N, ld0 and the epilogue strides multiples of 4: host-checked).
+template <int EPI, int FMT>
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, GemmEpi ep) {
+  const int n4 = N >> 2;
+  const size_t total = (size_t)M * n4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), c = (int)(i - (size_t)m * n4) * 4;
+    f32x4 v = *(const f32x4*)(part + (size_t)m * N + c);
+    for (int s = 1; s < S; ++s) v += *(const f32x4*)(part + ((size_t)s * M + m) * N + c);
+    if (ep.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += ep.bias[c + r];
+    }
+    const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
+    epi_store4<EPI, FMT>(ep, orow, c, v);
   }
 }
 

@@ -21,19 +21,20 @@ def main():
     groups = defaultdict(list)
     for r in rows:
         name = r.get("Kernel_Name", "")
-        if "gemm_pingpong" not in name and "gemm_planar" not in name:
+        if not any(k in name for k in ("gemm_pingpong", "gemm_planar", "splitk_reduce")):
             continue
+        kind = "pp" if "gemm_pingpong" in name else "pl" if "gemm_planar" in name else "red"
         wg = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 0)) or 0)
         grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
         blocks = grid // wg if wg else 0
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # us
         epi = name.split("kernel<")[1].split(",")[0] if "kernel<" in name else "?"
-        groups[(epi, blocks)].append(dur)
+        groups[(kind, epi, blocks)].append(dur)
     out = []
-    for (epi, blocks), durs in sorted(groups.items()):
+    for (kind, epi, blocks), durs in sorted(groups.items()):
         rounds = math.ceil(blocks / 256) if blocks else 0
         mean = sum(durs) / len(durs)
-        out.append({"epi": epi, "blocks": blocks, "dispatches": len(durs), "rounds": rounds,
+        out.append({"kernel": kind, "epi": epi, "blocks": blocks, "dispatches": len(durs), "rounds": rounds,
                     "fill_last_round": round(blocks / 256 - (rounds - 1), 3) if rounds else 0,
                     "mean_us": round(mean, 1), "us_per_round": round(mean / rounds, 1) if rounds else 0,
                     "total_ms": round(sum(durs) / 1e3, 2)})

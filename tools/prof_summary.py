@@ -36,8 +36,10 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16", "gemm_planar_kernel": "planar"}
-PLANAR_FMT = {"1": "x2f16", "2": "bf16"}  # gemm_planar_kernel<EPI, Tile, FMT, ...>
+FAMILIES = {"gemm_f32_nt_kernel": "f32", "gemm_x3bf16_nt_kernel": "x3bf16", "gemm_planar_kernel": "planar",
+            "gemm_pingpong_kernel": "pingpong"}
+PLANAR_FMT = {"1": "x2f16", "2": "bf16"}  # gemm_planar_kernel<EPI, Tile, FMT, ...>, gemm_pingpong_kernel<EPI, FMT, ...>
+FMT_ARG = {"planar": 2, "pingpong": 1}
 
 
 def gemm_variant(name):
@@ -45,7 +47,7 @@ def gemm_variant(name):
     for k, fam in FAMILIES.items():
         if k + "<" in name:
             args = name.split(k + "<")[1]
-            if fam == "planar":  # the third template argument is the activation format
+            if fam in FMT_ARG:  # the activation-format template argument
                 depth, parts, cur = 0, [], ""
                 for ch in args:
                     if ch == "<":
@@ -60,7 +62,7 @@ def gemm_variant(name):
                     else:
                         cur += ch
                 parts.append(cur.strip())
-                fam = PLANAR_FMT.get(parts[2], "planar")
+                fam = PLANAR_FMT.get(parts[FMT_ARG[fam]], fam)
             return fam, args[0]
     return None
 
