@@ -181,16 +181,18 @@ def main():
         return cie
 
     def timed(warmup, steps, profile):
-        for _ in range(warmup):
+        for i in range(warmup):
             step()
+            log(f"[rank {rank}] warmup step {i + 1}/{warmup}")
         if profile:
             model.profile(True)  # HIP events around every GEMM launch of the timed region
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for i in range(steps):
             cie = step()
+            log(f"[rank {rank}] step {i + 1}/{steps}")  # progress (long configs); host-side only
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
