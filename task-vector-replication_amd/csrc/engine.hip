@@ -262,6 +262,108 @@ int act_fmt(const tvr_model* m) {
   return m->gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : m->gemm_mode == TVR_GEMM_BF16 ? ACT_BF16 : ACT_F32;
 }
 
+// gemm_pingpong_kernel over tiles [tile_base, tile_base + count) of a planar
+// launch's raster (count 0: all), VEC epilogue
+void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
+               const GemmEpi& ep0, float acc_scale, int tile_base, int count, hipStream_t st) {
+  GemmEpi ep = ep0;
+  ep.tile_base = tile_base;
+  ep.tile_count = count;
+  const dim3 g(count > 0 ? count : gemm_pingpong_grid(M, N));
+#define TVR_PP1(E, F) \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
+                     ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_PP1F(E) \
+  if (a_fmt == ACT_X2F16) { TVR_PP1(E, ACT_X2F16); } else { TVR_PP1(E, ACT_BF16); }
+  switch (epi) {
+    case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
+    case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
+    default: TVR_PP1F(EPI_RESID); break;
+  }
+#undef TVR_PP1F
+#undef TVR_PP1
+}
+
+// The same tiles with K split over `ksplit` blocks per tile: fp32 partial
+// tiles to the model's split-K workspace, then splitk_reduce_kernel sums them
+// in order and applies the epilogue (deterministic).
+int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
+                     const GemmEpi& ep, float acc_scale, int tile_base, int count, int ksplit, tvr_model* m,
+                     hipStream_t st) {
+  const int rc = ensure_splitk(m, (size_t)ksplit * count * PP_TILE_ELEMS * sizeof(float), st);
+  if (rc != TVR_OK) return rc;
+  GemmEpi pe{};
+  pe.out0 = m->splitk_ws;
+  pe.a_rows = ep.a_rows;
+  pe.k_split = ksplit;
+  pe.tile_base = tile_base;
+  pe.tile_count = count;
+  const dim3 g(count * ksplit), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
+  if (a_fmt == ACT_X2F16)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+#define TVR_SK_REDUCE(E, F)                                                                                     \
+  hipLaunchKernelGGL((splitk_reduce_kernel<E, F>), rg, dim3(256), 0, st, (const float*)m->splitk_ws, ksplit, \
+                     tile_base, count, M, N, ep)
+#define TVR_SK_REDUCE_F(E) \
+  if (a_fmt == ACT_X2F16) { TVR_SK_REDUCE(E, ACT_X2F16); } else { TVR_SK_REDUCE(E, ACT_BF16); }
+  switch (epi) {
+    case EPI_BIAS: TVR_SK_REDUCE_F(EPI_BIAS); break;
+    case EPI_SPLIT_GELU_ACT: TVR_SK_REDUCE_F(EPI_SPLIT_GELU_ACT); break;
+    default: TVR_SK_REDUCE_F(EPI_RESID); break;
+  }
+#undef TVR_SK_REDUCE_F
+#undef TVR_SK_REDUCE
+  return TVR_OK;
+}
+
+// Launch shape of a planar GEMM on 256 CUs (gemm_pingpong_kernel, one block
+// per CU): fewer than 192 tiles -> split-K over the whole launch; otherwise,
+// when the last round would run partly empty, its tiles (the raster's last
+// ones) go to a second launch with split-K, ceil(T S / 256) / S rounds instead
+// of one, if the round time saved beats the partial tiles' HBM round trip.
+struct PpPlan {
+  int ksplit = 1;    // whole launch
+  int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
+  int tail_split = 1;
+};
+bool gemm_tail_enabled() {
+  static const bool on = env_flag("TVR_GEMM_TAIL");
+  return on;
+}
+PpPlan plan_pp(int M, int N, int K, int a_fmt) {
+  PpPlan p;
+  const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_BF16 ? 64 : 32);
+  if (tiles < 192) {
+    p.ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
+    return p;
+  }
+  const int rounds = (tiles + 255) / 256;
+  const int tb = tiles - 256 * (rounds - 1);
+  if (rounds < 2 || tb > 224 || !gemm_tail_enabled()) return p;
+  int best = 1;
+  double br = 1.0;
+  for (int s = 2; s <= 16 && nkt / s >= 8; ++s) {
+    const double r = std::ceil(tb * (double)s / 256.0) / s;
+    if (r < br - 1e-9) {
+      br = r;
+      best = s;
+    }
+  }
+  if (best < 2) return p;
+  const double round_us = nkt * 2.5;  // ~2.3-2.7 us per k-tile per block (profiles/gemm_pingpong_anatomy_r01.jsonl)
+  const double saved_us = (1.0 - br) * round_us;
+  const double cost_us = (best + 1.0) * tb * (double)PP_TILE_ELEMS * 8.0 / 5.0e6;  // partials written + read, ~5 TB/s
+  if (saved_us > 1.5 * cost_us + 10.0) {
+    p.tail_base = 256 * (rounds - 1);
+    p.tail_split = best;
+  }
+  return p;
+}
+
 // C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] (a_fmt ACT_F32) or a
 // planar activation format (split.hpp: lda logical elements per row), which
 // needs the same format's weight planes (W.h) and runs gemm_planar_kernel.
@@ -331,42 +433,18 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   }
 #define TVR_GEMM_PICK(E) \
   if (planar) { TVR_PL_LAUNCH(E); } else { TVR_GEMM_PICK_NP(E); }
-  // Split-K: a planar launch of fewer than 192 256x256 tiles (the clean
-  // forward's 180-row GEMMs, layer sweeps) cannot fill 256 CUs; its K range is
-  // split so tiles x splits fills them, each split writes an fp32 partial
-  // product and splitk_reduce_kernel sums the splits in order and applies the
-  // epilogue (deterministic; a different summation order than one block).
-  int ksplit = 1;
-  if (planar && pingpong && m && vec && gemm_splitk_enabled()) {
-    const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_BF16 ? 64 : 32);
-    if (tiles < 192) ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
-  }
-  if (ksplit > 1) {
-    const int rc = ensure_splitk(m, (size_t)ksplit * M * N * sizeof(float), st);
+  // planar launches on the pingpong kernel with a model: split-K / tail split (plan_pp)
+  PpPlan plan;
+  if (planar && pingpong && m && vec && gemm_splitk_enabled()) plan = plan_pp(M, N, K, a_fmt);
+  if (plan.ksplit > 1) {
+    const int rc = launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0,
+                                    gemm_pingpong_grid(M, N), plan.ksplit, m, st);
     if (rc != TVR_OK) return rc;
-    GemmEpi pe{};
-    pe.out0 = m->splitk_ws;
-    pe.ld0 = N;
-    pe.a_rows = ep.a_rows;
-    pe.k_split = ksplit;
-    const dim3 g(gemm_pingpong_grid(M, N) * ksplit), rg(std::min(2048, (M * (N / 4) + 255) / 256));
-    if (a_fmt == ACT_X2F16)
-      hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
-                         (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
-    else
-      hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
-                         (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
-#define TVR_SK_REDUCE(E, F) \
-  hipLaunchKernelGGL((splitk_reduce_kernel<E, F>), rg, dim3(256), 0, st, (const float*)m->splitk_ws, ksplit, M, N, ep)
-#define TVR_SK_REDUCE_F(E) \
-  if (a_fmt == ACT_X2F16) { TVR_SK_REDUCE(E, ACT_X2F16); } else { TVR_SK_REDUCE(E, ACT_BF16); }
-    switch (epi) {
-      case EPI_BIAS: TVR_SK_REDUCE_F(EPI_BIAS); break;
-      case EPI_SPLIT_GELU_ACT: TVR_SK_REDUCE_F(EPI_SPLIT_GELU_ACT); break;
-      default: TVR_SK_REDUCE_F(EPI_RESID); break;
-    }
-#undef TVR_SK_REDUCE_F
-#undef TVR_SK_REDUCE
+  } else if (plan.tail_base > 0) {
+    launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, st);
+    const int rc = launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
+                                    gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st);
+    if (rc != TVR_OK) return rc;
   } else
   switch (epi) {
     case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;

@@ -71,11 +71,14 @@ struct GemmEpi {
   // Diagnostics only (tools/gemm_probe.hip; the engine passes nullptr): per
   // block {Δs_memtime, Δs_memrealtime} to read the shader clock under load.
   unsigned long long* stamps;
-  // gemm_pingpong_kernel split-K (engine: small-M launches): > 1 runs
-  // tiles x k_split blocks, each writing its fp32 partial product to
-  // out0 + split * M * ld0 (EPI_BIAS, bias nullptr); splitk_reduce_kernel sums
-  // the splits in order and applies the real epilogue.
+  // gemm_pingpong_kernel launch shape (engine: small launches, last rounds):
+  // tiles [tile_base, tile_base + tile_count) of the grouped raster (count 0:
+  // all); k_split > 1 runs count x k_split blocks, each writing its fp32
+  // partial tile to out0 + (split * count + tile) * 256 * 256 (EPI_BIAS, bias
+  // nullptr), which splitk_reduce_kernel sums in order under the real epilogue.
   int k_split;
+  int tile_base;
+  int tile_count;
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":

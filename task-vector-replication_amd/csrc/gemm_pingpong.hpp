@@ -42,8 +42,22 @@
 namespace tvr {
 
 constexpr int PP_THREADS = 512;
+constexpr int PP_TILE_ELEMS = 256 * 256;  // one tile's fp32 partial product (split-K workspace unit)
 
 inline int gemm_pingpong_grid(int M, int N) { return ((M + 255) / 256) * ((N + 255) / 256); }
+
+// Tile wg of the grouped raster: GEMM_GROUP_M m-blocks walked fastest, then
+// the next column of blocks (blocks b and b + 8 of a launch share an XCD
+// after the remap, so neighbours share A rows / W columns in one L2).
+__host__ __device__ inline void pp_tile_coords(int wg, int nbm, int nbn, int& m0, int& n0) {
+  const int per_group = GEMM_GROUP_M * nbn;
+  const int grp = wg / per_group;
+  const int first_m = grp * GEMM_GROUP_M;
+  const int gsz = nbm - first_m < GEMM_GROUP_M ? nbm - first_m : GEMM_GROUP_M;
+  const int in_grp = wg - grp * per_group;
+  m0 = (first_m + in_grp % gsz) * 256;
+  n0 = (in_grp / gsz) * 256;
+}
 
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
@@ -72,18 +86,17 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF + 512];
 
   const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
-  const int S = ep.k_split > 1 ? ep.k_split : 1;  // split-K: block = (tile, split)
-  const int nwg = nbm * nbn * S;
+  // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
+  // each split over S k-ranges (block = (tile, split))
+  const int S = ep.k_split > 1 ? ep.k_split : 1;
+  const int count = ep.tile_count > 0 ? ep.tile_count : nbm * nbn;
+  const int nwg = count * S;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgs = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int wg = wgs / S, split = wgs - wg * S;
-  const int per_group = GEMM_GROUP_M * nbn;
-  const int grp = wg / per_group;
-  const int first_m = grp * GEMM_GROUP_M;
-  const int gsz = min(nbm - first_m, GEMM_GROUP_M);
-  const int in_grp = wg - grp * per_group;
-  const int m0 = (first_m + in_grp % gsz) * 256, n0 = (in_grp / gsz) * 256;
+  const int lt = wgs / S, split = wgs - lt * S;
+  int m0, n0;
+  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0);
 
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
@@ -257,10 +270,11 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
   }
-  if (S > 1) {  // partial product of this split (EPI_BIAS launches only; host-checked)
+  if (S > 1) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
     GemmEpi pe = ep;
-    pe.out0 = ep.out0 + (size_t)split * M * ep.ld0;
-    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+    pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
+    pe.ld0 = 256;
+    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M - m0, N - n0, wr * 128, wc * 64, lane);
   } else {
     gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
   }
@@ -276,18 +290,24 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   }
 }
 
-// Sum of the k_split partial products [S][M][N] (fixed order: deterministic)
-// + bias, then the launch's real epilogue on four consecutive columns per
-// thread (N, ld0 and the epilogue strides multiples of 4: host-checked).
+// Sum of the k_split partial tiles [S][count][256][256] (fixed order:
+// deterministic) + bias, then the launch's real epilogue on four consecutive
+// columns per thread (N, ld0 and the epilogue strides multiples of 4:
+// host-checked).  Tiles [tile_base, tile_base + count) of the raster.
 template <int EPI, int FMT>
 __global__ void __launch_bounds__(256)
-splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N, GemmEpi ep) {
-  const int n4 = N >> 2;
-  const size_t total = (size_t)M * n4;
+splitk_reduce_kernel(const float* __restrict__ part, int S, int tile_base, int count, int M, int N, GemmEpi ep) {
+  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
+  const size_t total = (size_t)count * (PP_TILE_ELEMS / 4);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int m = (int)(i / n4), c = (int)(i - (size_t)m * n4) * 4;
-    f32x4 v = *(const f32x4*)(part + (size_t)m * N + c);
-    for (int s = 1; s < S; ++s) v += *(const f32x4*)(part + ((size_t)s * M + m) * N + c);
+    const int lt = (int)(i / (PP_TILE_ELEMS / 4)), e = (int)(i % (PP_TILE_ELEMS / 4)) * 4;
+    int m0, n0;
+    pp_tile_coords(tile_base + lt, nbm, nbn, m0, n0);
+    const int m = m0 + (e >> 8), c = n0 + (e & 255);
+    if (m >= M || c >= N) continue;
+    const float* p = part + (size_t)lt * PP_TILE_ELEMS + e;
+    f32x4 v = *(const f32x4*)p;
+    for (int s = 1; s < S; ++s) v += *(const f32x4*)(p + (size_t)s * count * PP_TILE_ELEMS);
     if (ep.bias) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += ep.bias[c + r];
