@@ -106,6 +106,30 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x * (x >= 0.0f ? 1.0f - h : h);
 }
 
+// gelu_erf on two values with packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32:
+// the polynomial at half the VALU issue cycles); identical arithmetic.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752440f;
+  const f32x2 d = __builtin_elementwise_fma(z, f32x2{0.5f, 0.5f}, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = {0.17087277f, 0.17087277f};
+#define TVR_G2(c) p = __builtin_elementwise_fma(p, t, f32x2{c, c})
+  TVR_G2(-0.82215223f);
+  TVR_G2(1.48851587f);
+  TVR_G2(-1.13520398f);
+  TVR_G2(0.27886807f);
+  TVR_G2(-0.18628806f);
+  TVR_G2(0.09678418f);
+  TVR_G2(0.37409196f);
+  TVR_G2(1.00002368f);
+  TVR_G2(-1.26551223f);
+#undef TVR_G2
+  const f32x2 a = __builtin_elementwise_fma(-z, z, p) * 1.44269504088896341f;
+  const f32x2 h = 0.5f * t * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  return x * f32x2{x.x >= 0.0f ? 1.0f - h.x : h.x, x.y >= 0.0f ? 1.0f - h.y : h.y};
+}
+
 // One output element of the fused epilogues (v = acc + bias already); FMT is
 // the activation format of EPI_SPLIT_GELU_ACT's GELU columns.
 template <int EPI, int FMT = ACT_X2F16>

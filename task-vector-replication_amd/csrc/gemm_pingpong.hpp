@@ -59,12 +59,79 @@ __host__ __device__ inline void pp_tile_coords(int wg, int nbm, int nbn, int& m0
   n0 = (in_grp / gsz) * 256;
 }
 
+// Epilogue through LDS (after the K loop, the staging buffers are free): the
+// accumulators' natural layout gives each store instruction 16 rows x 32-64 B
+// (a 16-column slice per row; 32 B per plane for the split activation format),
+// and 256 lockstep blocks writing such partial lines ran the QKV+MLP-in
+// epilogue at half the HBM write rate of full lines.  Here each 128-row half
+// of the tile goes to LDS (row stride 260 floats: conflict-free 16-B writes),
+// then all 512 threads store whole rows: 1 KB (fp32) or 2 x 512 B (planes)
+// contiguous per row.  Rows [row0, row0 + Mlim) / columns [col0, col0 + Nlim)
+// of the output; ep's out0 / out1h / resid / out_rows / bias index globally.
+constexpr int PP_EPI_LDR = 260;                   // floats per LDS row
+constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
+
+template <int EPI, int FMT>
+__device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (&acc)[8][4], float* L, int row0,
+                                                int col0, int Mlim, int Nlim, int wr, int wc, int lane, int t,
+                                                float acc_scale) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if (wr == p) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *(f32x4*)(L + (i * 16 + (lane & 15)) * PP_EPI_LDR + wc * 64 + j * 16 + 4 * (lane >> 4)) =
+              acc[i][j] * acc_scale;
+    }
+    __syncthreads();
+    const int rows = min(128, Mlim - p * 128);
+    bool split8 = false;
+    if constexpr (EPI == EPI_SPLIT_GELU_ACT) split8 = col0 >= ep.n_split && Nlim >= 256;
+    if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
+      for (int it = t; it < 128 * 32; it += PP_THREADS) {
+        const int r = it >> 5, c = (it & 31) * 8;
+        if (r >= rows) continue;
+        const float* src = L + r * PP_EPI_LDR + c;
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[k] + (ep.bias ? ep.bias[col0 + c + k] : 0.f);
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const f32x2 g = gelu_erf2(f32x2{v[k], v[k + 1]});
+          v[k] = g.x;
+          v[k + 1] = g.y;
+        }
+        const int m = row0 + p * 128 + r;
+        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
+        store_act8<FMT>(ep.out1h + orow * ep.ld1h + (col0 + c - ep.n_split), ep.ps1h, v, ep.range_flag);
+      }
+    } else {
+      for (int it = t; it < 128 * 64; it += PP_THREADS) {
+        const int r = it >> 6, c = (it & 63) * 4;
+        if (r >= rows || c >= Nlim) continue;
+        f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c);
+        if (ep.bias) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] += ep.bias[col0 + c + k];
+        }
+        const int m = row0 + p * 128 + r;
+        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
+        epi_store4<EPI, FMT>(ep, orow, col0 + c, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
 // (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
 // waits in the loop (racy: timing only), 5 LDS-DMA issued inside the MFMA
 // clusters instead of the read segments, 6 per-block stamps (start, loop
-// start, loop end, end) of wave 0 to ep.stamps[4 block + i].
+// start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
+// epilogue (no LDS pass).
 template <int EPI, int FMT, bool VEC = true, int VAR = 0>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
@@ -81,9 +148,10 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   constexpr int BUF = 2 * NPL * PL;    // halves per buffer: A planes, then W planes
   constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
   static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
-  static_assert((2 * BUF + 512) * 2 <= 160 * 1024, "LDS budget");
+  constexpr int LDS_HALVES = (2 * BUF + 512) > PP_EPI_LDS ? (2 * BUF + 512) : PP_EPI_LDS;
+  static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
   // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF + 512];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_HALVES];
 
   const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
   // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
@@ -264,6 +332,26 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sink's DMAs retire before the block ends
 
+  if constexpr (VEC && VAR != 7) {  // epilogue through LDS (VAR 7: the register epilogue, for A/B)
+    __syncthreads();  // every wave's DMA retired (vmcnt(0) above) and last LDS reads done
+    float* L = reinterpret_cast<float*>(lds);
+    if (S > 1) {
+      GemmEpi pe = ep;
+      pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
+      pe.ld0 = 256;
+      pp_epilogue_lds<EPI, FMT>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+    } else {
+      pp_epilogue_lds<EPI, FMT>(ep, acc, L, m0, n0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+    }
+    if (VAR == 6 && ep.stamps && t == 0) {
+      unsigned long long* o = ep.stamps + 4 * blockIdx.x;
+      o[0] = st0;
+      o[1] = d_loop0;
+      o[2] = d_loop1;
+      o[3] = __builtin_amdgcn_s_memtime();
+    }
+    return;
+  }
   if (acc_scale != 1.0f) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)

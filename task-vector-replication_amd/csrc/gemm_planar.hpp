@@ -96,8 +96,9 @@ __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n
     if (n0 < ep.n_split) {  // n_split % 4 == 0: a group never straddles it
       *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v;
     } else {
-      store_act4<FMT>(ep.out1h + orow * ep.ld1h + (n0 - ep.n_split), ep.ps1h, gelu_erf(v[0]), gelu_erf(v[1]),
-                      gelu_erf(v[2]), gelu_erf(v[3]), ep.range_flag);
+      const f32x2 g01 = gelu_erf2(f32x2{v[0], v[1]}), g23 = gelu_erf2(f32x2{v[2], v[3]});
+      store_act4<FMT>(ep.out1h + orow * ep.ld1h + (n0 - ep.n_split), ep.ps1h, g01.x, g01.y, g23.x, g23.y,
+                      ep.range_flag);
     }
   } else {
     static_assert(EPI == EPI_RESID, "planar epilogues: bias, split-GELU (activation format), residual");

@@ -68,6 +68,30 @@ __device__ __forceinline__ void store_act4(uint16_t* p, int plane, float a, floa
   }
 }
 
+// eight consecutive elements (p 16-B aligned): one 16-B store per plane
+template <int FMT>
+__device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (&v)[8], unsigned* flag) {
+  if constexpr (FMT == ACT_X2F16) {
+    unsigned lo[4], hi[4];
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const SplitF16 x = split_f16(v[2 * k]), y = split_f16(v[2 * k + 1]);
+      lo[k] = x.h0 | ((unsigned)y.h0 << 16);
+      hi[k] = x.h1 | ((unsigned)y.h1 << 16);
+      m = fmaxf(m, fmaxf(fabsf(v[2 * k]), fabsf(v[2 * k + 1])));
+    }
+    *(uint4*)p = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    *(uint4*)(p + plane) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    if (m * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
+  } else {
+    unsigned w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = bf16_bits(v[2 * k]) | ((unsigned)bf16_bits(v[2 * k + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // fp32 rows a [rows][lda] -> activation format FMT with K logical columns
 template <int FMT>
 __global__ void act_rows_kernel(const float* __restrict__ a, int lda, uint16_t* __restrict__ out, int rows, int K,

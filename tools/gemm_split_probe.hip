@@ -149,16 +149,22 @@ int main(int argc, char** argv) {
                                       : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
           hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2ppg") {  // pingpong with the QKV+MLP-in epilogue, timed
+        } else if (path == "x2ppg" || path == "x2ppg7") {  // pingpong with the QKV+MLP-in epilogue, timed
           grid = gemm_pingpong_grid(s.M, s.N);
           GemmEpi eg = ee;
-          eg.n_split = (s.N * 3 / 7) & ~3;
+          eg.n_split = (s.N * 3 / 7) & ~255;
           eg.out1h = (uint16_t*)(C) + eg.n_split;
           eg.ld1h = 2 * s.N;
           eg.ps1h = s.N;
           eg.range_flag = flag;
-          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 0>), dim3(grid), dim3(PP_THREADS),
+          auto kg = path == "x2ppg" ? gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 0>
+                                    : gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 7>;
+          hipLaunchKernelGGL(kg, dim3(grid), dim3(PP_THREADS),
                              0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+        } else if (path == "x2pp7") {  // register epilogue (EPI_BIAS)
+          grid = gemm_pingpong_grid(s.M, s.N);
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 7>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2pp6" || path == "x2pp6g") {  // per-block anatomy (prologue / loop / epilogue)
           grid = gemm_pingpong_grid(s.M, s.N);
           GemmEpi eg = ee;
