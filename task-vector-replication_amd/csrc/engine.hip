@@ -264,11 +264,18 @@ int act_fmt(const tvr_model* m) {
 
 // gemm_pingpong_kernel over tiles [tile_base, tile_base + count) of a planar
 // launch's raster (count 0: all), VEC epilogue
+// Raster group (m-blocks walked before the next block column): 4, or 2 when
+// there are at most 16 block columns (tools/gemm_split_probe x2ppgm<N>: at
+// M = 90,000 the qkv shape ran 459 / 451 / 419 TF at 4 / 8 / 16, the
+// MLP-out shape (10 columns) 470 / 466 / 458 at 2 / 4 / 8).
+int pp_group_m(int N) { return (N + 255) / 256 <= 16 ? 2 : 4; }
+
 void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
                const GemmEpi& ep0, float acc_scale, int tile_base, int count, hipStream_t st) {
   GemmEpi ep = ep0;
   ep.tile_base = tile_base;
   ep.tile_count = count;
+  ep.group_m = pp_group_m(N);
   const dim3 g(count > 0 ? count : gemm_pingpong_grid(M, N));
 #define TVR_PP1(E, F) \
   hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
@@ -288,11 +295,14 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
 // tiles to the model's split-K workspace, then splitk_reduce_kernel sums them
 // in order and applies the epilogue (deterministic).
 int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
-                     const GemmEpi& ep, float acc_scale, int tile_base, int count, int ksplit, tvr_model* m,
+                     const GemmEpi& ep0, float acc_scale, int tile_base, int count, int ksplit, tvr_model* m,
                      hipStream_t st) {
   const int rc = ensure_splitk(m, (size_t)ksplit * count * PP_TILE_ELEMS * sizeof(float), st);
   if (rc != TVR_OK) return rc;
+  GemmEpi ep = ep0;  // the reduce's epilogue: same raster as the partial launch
+  ep.group_m = pp_group_m(N);
   GemmEpi pe{};
+  pe.group_m = ep.group_m;
   pe.out0 = m->splitk_ws;
   pe.a_rows = ep.a_rows;
   pe.k_split = ksplit;

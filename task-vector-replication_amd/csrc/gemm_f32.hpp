@@ -79,6 +79,7 @@ struct GemmEpi {
   int k_split;
   int tile_base;
   int tile_count;
+  int group_m;  // gemm_pingpong_kernel raster: m-blocks per group (0: GEMM_GROUP_M)
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":

@@ -49,11 +49,11 @@ inline int gemm_pingpong_grid(int M, int N) { return ((M + 255) / 256) * ((N + 2
 // Tile wg of the grouped raster: GEMM_GROUP_M m-blocks walked fastest, then
 // the next column of blocks (blocks b and b + 8 of a launch share an XCD
 // after the remap, so neighbours share A rows / W columns in one L2).
-__host__ __device__ inline void pp_tile_coords(int wg, int nbm, int nbn, int& m0, int& n0) {
-  const int per_group = GEMM_GROUP_M * nbn;
+__host__ __device__ inline void pp_tile_coords(int wg, int nbm, int nbn, int& m0, int& n0, int gm = GEMM_GROUP_M) {
+  const int per_group = gm * nbn;
   const int grp = wg / per_group;
-  const int first_m = grp * GEMM_GROUP_M;
-  const int gsz = nbm - first_m < GEMM_GROUP_M ? nbm - first_m : GEMM_GROUP_M;
+  const int first_m = grp * gm;
+  const int gsz = nbm - first_m < gm ? nbm - first_m : gm;
   const int in_grp = wg - grp * per_group;
   m0 = (first_m + in_grp % gsz) * 256;
   n0 = (in_grp / gsz) * 256;
@@ -164,7 +164,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   const int wgs = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int lt = wgs / S, split = wgs - lt * S;
   int m0, n0;
-  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0);
+  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M);
 
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
@@ -390,7 +390,7 @@ splitk_reduce_kernel(const float* __restrict__ part, int S, int tile_base, int c
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int lt = (int)(i / (PP_TILE_ELEMS / 4)), e = (int)(i % (PP_TILE_ELEMS / 4)) * 4;
     int m0, n0;
-    pp_tile_coords(tile_base + lt, nbm, nbn, m0, n0);
+    pp_tile_coords(tile_base + lt, nbm, nbn, m0, n0, ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M);
     const int m = m0 + (e >> 8), c = n0 + (e & 255);
     if (m >= M || c >= N) continue;
     const float* p = part + (size_t)lt * PP_TILE_ELEMS + e;

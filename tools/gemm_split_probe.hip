@@ -161,6 +161,12 @@ int main(int argc, char** argv) {
                                     : gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 7>;
           hipLaunchKernelGGL(kg, dim3(grid), dim3(PP_THREADS),
                              0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+        } else if (path.rfind("x2ppgm", 0) == 0) {  // raster group size: x2ppgm<N>
+          grid = gemm_pingpong_grid(s.M, s.N);
+          GemmEpi eg = ee;
+          eg.group_m = std::stoi(path.substr(6));
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
         } else if (path == "x2pp7") {  // register epilogue (EPI_BIAS)
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 7>), dim3(grid), dim3(PP_THREADS), 0, 0,
