@@ -433,6 +433,35 @@ def test_pythia160m_shape_cie_subset(tokenizer, gemm):
         assert rel_err(out["logits"][i], oracle.forward(torch.tensor([p]))[0, -1]) < 1e-4
 
 
+@pytest.mark.slow
+def test_gemm_launch_shapes_full_cie_match_fp32_kernel(tokenizer):
+    """Every GEMM launch shape of the engine's planar path in one sweep: a full
+    Pythia-160m-shape CIE (12 x 12 sites, 12 prompts) runs launches from 6 to
+    ~2,100 tiles, i.e. split-K (< 192 tiles), plain multi-round launches and
+    the last-round tail split (engine.hip plan_pp), all on gemm_pingpong_kernel
+    with the LDS epilogue.  Checked against the same sweep on the independent
+    fp32-MFMA kernel family (gemm_f32_nt_kernel) at the north star's
+    tolerance, and clean probabilities likewise."""
+    cfg = tvr_amd.get_config("pythia-160m")
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
+    prompts = answers = None
+    res = {}
+    for gemm in ("x2f16", "f32"):
+        model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", gemm=gemm)
+        if prompts is None:
+            prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, 12, 4, seed=99)
+        g = torch.Generator().manual_seed(5)
+        mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5
+        cie = tvr_amd.experiments.causal_indirect_effect_sums(mean.cuda(), prompts, answers, model)
+        p0 = model.forward_clean(prompts, targets=answers)["prob"]
+        res[gemm] = (cie.cpu().double(), p0.cpu().double())
+        del model
+        torch.cuda.empty_cache()
+    (c1, p1), (c2, p2) = res["x2f16"], res["f32"]
+    assert (c1 - c2).abs().max().item() <= 1e-4 * c2.abs().max().item() + 1e-9
+    assert (p1 - p2).abs().max().item() <= 1e-5 * p2.abs().max().item()
+
+
 def test_batched_fv_helpers_match_reference_loops(tiny_model, tiny_oracle, mean_pair):
     """check_accuracy_of_added_task_vector_by_layer and the head-count grid
     (scratch2.py:411-425) = the reference's per-cell loops on the oracle."""
