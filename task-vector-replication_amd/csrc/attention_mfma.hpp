@@ -58,9 +58,12 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   const int li = lane & 15, g = lane >> 4;
   constexpr int rd = CH, half = CH / 2;  // rotary_dim = d_head / 4
 
-  // row of absolute position j: the clean trace's prefix, or this run's rows
+  // row of absolute position j: the prefix (clean trace, or a shared-prefix
+  // leader's rows of this run), or this sequence's own rows
+  const float* pfx = sd.prefix_live ? qkv : cache;
+  const int ldp = sd.prefix_live ? ldq : ldc;
   auto row_of = [&](int j) -> const float* {
-    return j < sd.p0 ? cache + (size_t)(sd.cache_row + j) * ldc : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
+    return j < sd.p0 ? pfx + (size_t)(sd.cache_row + j) * ldp : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
   };
   // dims [g CH, g CH + CH) of a Q or K head row, rotated for position pos
   auto load_chunk = [&](const float* r, int pos, float (&x)[CH]) {

@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "tvr.h"
@@ -129,6 +131,7 @@ struct tvr_trace {
   float* z = nullptr;      // [L][max_tokens][d]
   float* qkv = nullptr;    // [L][max_tokens][3d]
   std::vector<int> seq_off, seq_len;
+  std::vector<int32_t> tokens;  // host copy of the traced ids (shared-prefix detection in patch sweeps)
   int n_seq = 0, n_tokens = 0;
 };
 
@@ -256,6 +259,9 @@ bool gemm_pp_small_enabled() {
   static const bool on = env_flag("TVR_GEMM_PP_SMALL");
   return on;
 }
+// TVR_PREFIX_SHARE=0 turns off shared-prefix rows in tvr_patch_sweep (A/B and
+// tests; read per call).
+bool prefix_share_enabled() { return env_flag("TVR_PREFIX_SHARE"); }
 
 // Activation format of the model's GEMM inputs (split.hpp).
 int act_fmt(const tvr_model* m) {
@@ -1069,6 +1075,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
                            hipMemcpyDeviceToDevice, st));
     trace->seq_off.assign(off.begin(), off.end());
     trace->seq_len.assign(seq_lens, seq_lens + n_seq);
+    trace->tokens.assign(tokens, tokens + R);
     trace->n_seq = n_seq;
     trace->n_tokens = R;
   }
@@ -1129,6 +1136,41 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
         return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": unknown kind");
     }
   }
+  // Shared prefixes (REPLACE_HEAD_ALLPOS): sites with the same (layer, head,
+  // vector) whose sequences start with the same tokens compute identical rows
+  // over that common prefix (position j attends to positions <= j only, and
+  // the patch is the same at every position).  The first such site (the
+  // leader) computes them; a follower starts at its common-prefix length P
+  // and reads positions < P's K/V from the leader's rows of this run
+  // (SeqDesc.prefix_live).  A CIE sweep's prompts all start with BOS, so
+  // (n_prompts - 1) / n_prompts of the position-0 rows — 1/T of the sweep's
+  // rows — are not recomputed.  The reference's batch-1 forwards compute that
+  // row identically for every prompt (scratch2.py:181-194).
+  std::vector<int> leader(n_sites, -1);
+  if (prefix_share_enabled() && (int)trace->tokens.size() >= trace->n_tokens) {
+    std::map<std::tuple<int, int, int, int>, int> first;
+    for (int i = 0; i < n_sites; ++i) {
+      const tvr_site& s = sites[i];
+      if (s.kind != TVR_SITE_REPLACE_HEAD_ALLPOS) continue;
+      const int32_t* tk = trace->tokens.data() + trace->seq_off[s.seq];
+      const auto key = std::make_tuple(s.layer, s.head, s.vec, (int)tk[0]);
+      const auto it = first.find(key);
+      if (it == first.end()) {
+        first.emplace(key, i);
+        continue;
+      }
+      const int ld = it->second;
+      const int32_t* tl = trace->tokens.data() + trace->seq_off[sites[ld].seq];
+      const int T = trace->seq_len[s.seq];
+      const int cap = std::min(T - 1, trace->seq_len[sites[ld].seq]);  // the last row stays the site's own
+      int P = 0;
+      while (P < cap && tk[P] == tl[P]) ++P;
+      if (P == 0) continue;
+      leader[i] = ld;
+      p0[i] = P;
+      nrow[i] = T - P;
+    }
+  }
   std::vector<int> order(n_sites);
   for (int i = 0; i < n_sites; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return entry[a] < entry[b]; });
@@ -1154,7 +1196,8 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     const int i = order[k];
     const tvr_site& s = sites[i];
     const int srow = trace->seq_off[s.seq];
-    seqs[k] = {row0[i], nrow[i], p0[i], srow, 0, 0};
+    seqs[k] = leader[i] >= 0 ? SeqDesc{row0[i], nrow[i], p0[i], row0[leader[i]], 0, 1}
+                             : SeqDesc{row0[i], nrow[i], p0[i], srow, 0, 0};
     EntryDesc e{};
     e.kind = s.kind;
     e.row0 = row0[i];

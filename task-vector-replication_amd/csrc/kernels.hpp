@@ -23,9 +23,10 @@ struct SeqDesc {
   int32_t row0;       // first computed row in the activation buffers
   int32_t n;          // number of computed rows
   int32_t p0;         // absolute position of row0
-  int32_t cache_row;  // trace row of position 0 (for the K/V prefix), -1: none
+  int32_t cache_row;  // row of position 0 for the K/V prefix (positions < p0), -1: none
   int32_t q0;         // first computed row that is a query (n-1: last row only)
-  int32_t pad;
+  int32_t prefix_live;  // 0: the prefix is in the clean trace (cache); 1: in this run's qkv rows
+                        // (a shared-prefix follower reads its leader's rows: tvr_patch_sweep)
 };
 
 // How a patch site's residual is materialised at its entry layer e
@@ -158,7 +159,8 @@ attention_kernel(const float* __restrict__ qkv, int ldq,
   const int d4 = dh >> 2;
   for (int e = t; e < T * d4; e += ATT_THREADS) {
     const int j = e / d4, k = (e - j * d4) * 4;
-    const float* src = (j < sd.p0) ? cache + (size_t)(sd.cache_row + j) * ldc
+    const float* src = (j < sd.p0) ? (sd.prefix_live ? qkv + (size_t)(sd.cache_row + j) * ldq
+                                                     : cache + (size_t)(sd.cache_row + j) * ldc)
                                    : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
     const float4 kv = *(const float4*)(src + d + h * dh + k);
     const float4 vv = *(const float4*)(src + 2 * d + h * dh + k);

@@ -410,6 +410,50 @@ def test_patch_sweep_site_kinds_against_hooks(tiny_model, tiny_oracle):
         assert abs(out["prob"][j].item() - pr) <= 1e-5 * torch.softmax(ref, 0).max().item()
 
 
+def test_patch_sweep_shared_prefix_rows(tiny_model, tiny_oracle, monkeypatch):
+    """Head-replacement sites on prompts that share prefixes (BOS only, 20
+    tokens, a whole duplicate prompt, none): followers read the prefix K/V
+    from their leader's rows (engine.hip tvr_patch_sweep).  Each site equals
+    the oracle's hook on its own prompt, and the sweep equals the same sweep
+    with sharing off (TVR_PREFIX_SHARE=0)."""
+    cfg = tiny_model.cfg
+    rng = random.Random(17)
+    base = [0] + [rng.randrange(1, cfg.d_vocab) for _ in range(29)]
+    prompts = [base[:24], base[:20] + [rng.randrange(1, cfg.d_vocab) for _ in range(7)], base[:24],
+               [5] + base[1:16], [0] + [rng.randrange(1, cfg.d_vocab) for _ in range(12)], base[:2]]
+    trace = tiny_model.trace(len(prompts), sum(map(len, prompts)))
+    tiny_model.forward_clean(prompts, trace=trace)
+    g = torch.Generator().manual_seed(4)
+    vecs = torch.randn(3, cfg.d_model, generator=g)
+    combos = [(0, 1, 0), (1, 3, 1), (0, 1, 2), (1, 3, 1)]  # (layer, head, vec); the last one twice
+    sites = tvr_amd.make_sites(len(prompts) * len(combos))
+    want = []
+    k = 0
+    tiny_oracle.cfg.use_attn_result = True
+    try:
+        for i, p in enumerate(prompts):
+            for l, h, v in combos:
+                s = sites[k]
+                s["seq"], s["kind"], s["target"] = i, tvr_amd._lib.SITE_REPLACE_HEAD_ALLPOS, p[1]
+                s["layer"], s["head"], s["vec"] = l, h, v
+                def hook(hv, hook, h=h, v=vecs[v]):
+                    hv[0, :, h, :] = v
+                    return hv
+                want.append(tiny_oracle.run_with_hooks(torch.tensor([p]), fwd_hooks=[
+                    (f"blocks.{l}.attn.hook_result", hook)])[0, -1])
+                k += 1
+    finally:
+        tiny_oracle.cfg.use_attn_result = False
+    out = tiny_model.patch_sweep(trace, sites, vecs.cuda(), topk=3, return_logits=True)
+    monkeypatch.setenv("TVR_PREFIX_SHARE", "0")
+    off = tiny_model.patch_sweep(trace, sites, vecs.cuda(), topk=3, return_logits=True)
+    for j, ref in enumerate(want):
+        assert rel_err(out["logits"][j], ref) < 1e-4, (j, sites[j])
+        assert out["topk"][j].tolist() == torch.topk(ref, 3).indices.tolist(), j
+    assert rel_err(out["logits"], off["logits"]) < 1e-5
+    assert torch.equal(out["topk"], off["topk"])
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("gemm", ["x2f16", "x3bf16", "f32"])
 def test_pythia160m_shape_cie_subset(tokenizer, gemm):
