@@ -998,13 +998,45 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
 
   std::vector<SeqDesc> seqs(n_seq);
   for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1, 0, 0};
+  std::vector<int32_t> tok(tokens, tokens + R);
+  // Shared prefixes without a trace (only each prompt's last row is read
+  // afterwards): a prompt whose leading tokens equal those of the first prompt
+  // with its first token computes only the rows after the common prefix and
+  // reads the prefix K/V from that prompt's rows (SeqDesc.prefix_live); every
+  // extraction prompt starts with BOS.  With a trace every row is kept (patch
+  // sweeps read any position of it).
+  if (!trace && prefix_share_enabled()) {
+    std::map<int, int> first;  // first token -> first prompt starting with it
+    std::vector<int32_t> ctok;
+    ctok.reserve(R);
+    int Rc = 0;
+    for (int s = 0; s < n_seq; ++s) {
+      const int T = seq_lens[s];
+      const int32_t* tk = tokens + off[s];
+      int P = 0, ld = -1;
+      const auto it = first.find(tk[0]);
+      if (it == first.end()) {
+        first.emplace(tk[0], s);
+      } else {
+        ld = it->second;
+        const int32_t* tl = tokens + off[ld];
+        const int cap = std::min(T - 1, seq_lens[ld]);
+        while (P < cap && tk[P] == tl[P]) ++P;
+      }
+      seqs[s] = P > 0 ? SeqDesc{Rc, T - P, P, seqs[ld].row0, 0, 1} : SeqDesc{Rc, T, 0, -1, 0, 0};
+      ctok.insert(ctok.end(), tk + P, tk + T);
+      last[s] = Rc + T - P - 1;
+      Rc += T - P;
+    }
+    tok.swap(ctok);
+    R = Rc;
+  }
   // without a trace only each prompt's last row is read after the last layer
   const bool trim = trace == nullptr;
   std::vector<SeqDesc> seqs_last(seqs);
   for (auto& q : seqs_last) q.q0 = q.n - 1;
   std::vector<int32_t> tg(n_seq, -1);
   if (targets) std::copy(targets, targets + n_seq, tg.begin());
-  std::vector<int32_t> tok(tokens, tokens + R);
 
   const int FC = std::min(kFinalChunk, n_seq);
   Carve cv;

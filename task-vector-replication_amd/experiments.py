@@ -47,8 +47,14 @@ EXTRACT_BATCH = 2048
 
 
 def _chunks(n: int, size: int):
-    for s in range(0, n, size):
-        yield s, min(n, s + size)
+    """[a, b) ranges of at most ``size`` covering range(n), as equal as
+    possible (12 prompts at 11 per launch run as 6 + 6, not 11 + 1: a
+    1-prompt launch shares no prefix rows and runs small GEMMs)."""
+    if n <= 0:
+        return
+    k = -(-n // size)
+    for i in range(k):
+        yield i * n // k, (i + 1) * n // k
 
 
 # ------------------------------------------------------------------ a1 / a2

@@ -227,6 +227,30 @@ def test_forward_clean_matches_oracle(tiny_model, tiny_oracle):
         assert out["topk"][i].tolist() == torch.topk(ref, 5).indices.tolist()
 
 
+def test_forward_clean_shared_prefix_rows(tiny_model, tiny_oracle, monkeypatch):
+    """Without a trace, prompts sharing leading tokens with an earlier prompt
+    compute only their own suffix rows (engine.hip tvr_forward_clean):
+    duplicates, 1-token prompts before and after longer ones, a prefix that
+    is a whole earlier prompt, different first tokens; last-row logits and
+    the z capture equal the oracle and the unshared run."""
+    cfg = tiny_model.cfg
+    rng = random.Random(23)
+    base = [0] + [rng.randrange(1, cfg.d_vocab) for _ in range(40)]
+    prompts = [[0], base[:30], base[:30], base[:12], base[:31] + [7, 9], [3] + base[1:20], [3] + base[1:5],
+               [0, 5], base[:2], [0] + [rng.randrange(1, cfg.d_vocab) for _ in range(17)]]
+    targets = [p[-1] for p in prompts]
+    out = tiny_model.forward_clean(prompts, targets=targets, topk=5, return_logits=True, capture=True)
+    for i, p in enumerate(prompts):
+        ref = tiny_oracle.forward(torch.tensor([p]))[0, -1]
+        assert rel_err(out["logits"][i], ref) < 1e-4, i
+        assert out["topk"][i].tolist() == torch.topk(ref, 5).indices.tolist(), i
+    monkeypatch.setenv("TVR_PREFIX_SHARE", "0")
+    off = tiny_model.forward_clean(prompts, targets=targets, topk=5, return_logits=True, capture=True)
+    assert rel_err(out["logits"], off["logits"]) < 1e-5
+    assert torch.equal(out["topk"], off["topk"])
+    assert rel_err(out["zsum"], off["zsum"]) < 1e-5
+
+
 def test_trace_matches_run_with_cache(tiny_model, tiny_oracle):
     prompts = ragged_prompts(5, tiny_model.cfg.d_vocab, 2)
     trace = tiny_model.trace(len(prompts), sum(map(len, prompts)))
