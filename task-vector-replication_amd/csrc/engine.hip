@@ -274,7 +274,14 @@ int act_fmt(const tvr_model* m) {
 // there are at most 16 block columns (tools/gemm_split_probe x2ppgm<N>: at
 // M = 90,000 the qkv shape ran 459 / 451 / 419 TF at 4 / 8 / 16, the
 // MLP-out shape (10 columns) 470 / 466 / 458 at 2 / 4 / 8).
-int pp_group_m(int N) { return (N + 255) / 256 <= 16 ? 2 : 4; }
+int pp_group_m(int N) {
+  static const int forced = [] {  // TVR_GEMM_GROUP=<g> forces one group size (A/B)
+    const char* e = getenv("TVR_GEMM_GROUP");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  if (forced > 0) return forced;
+  return (N + 255) / 256 <= 16 ? 2 : 4;
+}
 
 void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
                const GemmEpi& ep0, float acc_scale, int tile_base, int count, hipStream_t st) {
@@ -421,9 +428,11 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
                      st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
 #define TVR_PL_LAUNCH1(E, TL, F) \
   if (vec) TVR_PL_LAUNCH2(E, TL, F, true); else TVR_PL_LAUNCH2(E, TL, F, false)
+  GemmEpi epp = ep;  // whole-launch pingpong: the same raster group as launch_pp
+  epp.group_m = pp_group_m(N);
 #define TVR_PP_LAUNCH2(E, F, V)                                                                              \
   hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), dim3(gemm_pingpong_grid(M, N)), dim3(PP_THREADS), 0, st, \
-                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
+                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, epp)
 #define TVR_PL_LARGE(E, F)                                                   \
   if (pingpong) {                                                            \
     if (vec) TVR_PP_LAUNCH2(E, F, true); else TVR_PP_LAUNCH2(E, F, false);  \
