@@ -66,9 +66,11 @@ def parse():
     ap.add_argument("--model", default="pythia-2.8b")
     ap.add_argument("--prompts", type=int, default=12, help="CIE prompts per GPU per step")
     ap.add_argument("--kshot", type=int, default=4)
-    ap.add_argument("--extract", type=int, default=0,
-                    help="prompts for an (untimed) mean extraction; 0 = seeded random mean vectors, so every GEMM "
-                         "launch of the process belongs to a CIE step (rocprof averages == bench averages)")
+    ap.add_argument("--extract", type=int, default=2048,
+                    help="prompts of the mean extraction (a1, C2's N = 2048, 6-shot, T = 28) that supplies the CIE "
+                         "means; timed separately (extraction prompts/s, capture kernel GB/s); 0 = seeded random "
+                         "means, so every GEMM launch of the process belongs to a CIE step (the rocprof runs: "
+                         "rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
@@ -96,6 +98,31 @@ def pmc_summary(family, workload):
     if d.get("family") != family or d.get("workload") != workload:
         return None, None  # counters of another kernel or workload do not apply
     return d, f"{p.relative_to(ROOT)} ({d.get('source', '?')})"
+
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+
+
+def hbm_kernels(hbm, hbm_ex, steps):
+    """Achieved GB/s of the HBM-bound kernels (HIP events around each launch,
+    algorithmic bytes per include/tvr.h tvr_hbm_kind): injection, LayerNorm,
+    attention and target-probability rows from the timed CIE region; capture
+    from the timed extraction."""
+    out = {"peak_gbps": HBM_PEAK_GBPS,
+           "basis": "algorithmic bytes / summed HIP-event launch time (engine stream), per kernel kind"}
+
+    def row(v, per):
+        if not v["launches"]:
+            return None
+        g = v["gbps"]
+        return {"launches" + per: round(v["launches"] / (steps if per else 1), 1),
+                "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                "bytes_per_launch": round(v["bytes"] / v["launches"]),
+                "achieved_gbps": round(g, 1), "frac": round(g / HBM_PEAK_GBPS, 4)}
+    for k in ("entry", "lnpre", "attention", "row_stats"):
+        out[k] = row(hbm[k], "_per_step")
+    out["capture"] = row(hbm_ex["capture"], "") if hbm_ex else None
+    return out
 
 
 def log(*a):
@@ -154,17 +181,21 @@ def main():
     log(f"[rank {rank}] {args.model} synthetic weights on {dev} in {time.time() - t0:.1f}s")
 
     # --- mean head activations [L, H, d]: a real extraction (a1) or seeded random
-    te, n_ex = None, 0
+    te, n_ex, hbm_ex = None, 0, None
     if args.extract > 0:
         import random
         random.seed(4321)
         pairs = tvr_amd.tasks.synthetic_task(52, cfg.d_vocab, seed=7)
         ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, pairs, "→", ",", args.extract, 6)
+        sum_last_z(model, ex_prompts[:64])  # workspace sizing outside the timed extraction
         torch.cuda.synchronize()
+        model.profile(True)
         te = time.perf_counter()
         zsum = sum_last_z(model, ex_prompts)
         torch.cuda.synchronize()
         te = time.perf_counter() - te
+        hbm_ex = model.profile_hbm_stats()
+        model.profile(False)
         n_ex = len(ex_prompts)
         mean = model.project_heads(zsum) / n_ex
     else:
@@ -208,6 +239,7 @@ def main():
 
     # --- roofline of the dominant kernel, from the timed region's events
     st = model.profile_stats()
+    hbm = model.profile_hbm_stats()
     model.profile(False)
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
@@ -268,6 +300,7 @@ def main():
             "gemm_share_of_step": round(fam["ms"] / (elapsed * 1e3), 4),
             "variants": variants,
         },
+        "hbm_kernels": hbm_kernels(hbm, hbm_ex, args.steps),
         "algorithmic": {
             "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(value / world * f_alg / 1e12, 2),

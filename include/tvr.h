@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 4
+#define TVR_ABI_VERSION 5
 
 enum tvr_status {
   TVR_OK = 0,
@@ -250,6 +250,25 @@ typedef struct tvr_kernel_stats {
 } tvr_kernel_stats;
 int tvr_profile_enable(tvr_model* model, int32_t on);
 int tvr_profile_read(tvr_model* model, tvr_kernel_stats* out);
+
+/* The HBM-bound kernels, timed the same way (HIP events around each launch
+ * while profiling is enabled) with their algorithmic bytes: achieved GB/s =
+ * bytes / ms.  Index = enum tvr_hbm_kind. */
+enum tvr_hbm_kind {
+  TVR_HBM_ENTRY = 0,      /* patch injection at the entry layer (REPLACE_HEAD / ADD / SET_RESID):
+                           * clean rows in, patched rows out, z rows + W_O slice per head */
+  TVR_HBM_CAPTURE = 1,    /* extraction: sum of hook_z at every prompt's last row -> [d] per layer */
+  TVR_HBM_LNPRE = 2,      /* LayerNormPre rows -> GEMM input format */
+  TVR_HBM_ATTENTION = 3,  /* attention: fp32 Q/K/V rows in, z out (activation format [+ fp32 hook_z]) */
+  TVR_HBM_ROW_STATS = 4,  /* softmax target probability / top-k over one logit row per site */
+  TVR_HBM_KINDS = 5
+};
+typedef struct tvr_hbm_stats {
+  int64_t launches[5];
+  double ms[5];     /* summed launch durations */
+  double bytes[5];  /* algorithmic bytes summed */
+} tvr_hbm_stats;
+int tvr_profile_read_hbm(tvr_model* model, tvr_hbm_stats* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);
  * the weight planes of the split / bf16 modes are not included (X3BF16 6 B,

@@ -56,8 +56,16 @@ class CKernelStats(ctypes.Structure):
 
 GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
+
+class CHbmStats(ctypes.Structure):
+    _fields_ = [("launches", ctypes.c_int64 * 5), ("ms", ctypes.c_double * 5), ("bytes", ctypes.c_double * 5)]
+
+
+# include/tvr.h enum tvr_hbm_kind
+HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats")
+
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 4  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 5  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
@@ -109,6 +117,7 @@ SIGNATURES = {
                                        ctypes.c_void_p]),
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
+    "tvr_profile_read_hbm": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CHbmStats)]),
 }
 
 _LIB = None

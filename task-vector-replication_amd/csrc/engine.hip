@@ -117,7 +117,8 @@ struct tvr_model {
   float* splitk_ws = nullptr;  // split-K partial products (launch_gemm), grown on demand
   size_t splitk_bytes = 0;
   Staging staging;
-  // profiling (tvr_profile_enable): event pairs around GEMM launches
+  // profiling (tvr_profile_enable): event pairs around GEMM launches (kind =
+  // GEMM epilogue index 0-2) and the HBM-bound kernels (kind 3 + tvr_hbm_kind)
   bool prof = false;
   struct ProfRec { hipEvent_t a, b; int epi; double flops, bytes; };
   std::vector<ProfRec> prof_recs;
@@ -232,6 +233,31 @@ hipEvent_t prof_event(tvr_model* m) {
   }
   return e;
 }
+
+// HIP events around one HBM-bound launch (or a short launch sequence) while
+// profiling: done(kind, algorithmic bytes) records the closing event.
+struct ProfSpan {
+  tvr_model* m;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfSpan(tvr_model* m_, hipStream_t s) : m(m_), st(s) {
+    if (m && m->prof) {
+      a = prof_event(m);
+      b = prof_event(m);
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  void done(int kind, double bytes) {
+    if (!a || !b) return;
+    (void)hipEventRecord(b, st);
+    m->prof_recs.push_back({a, b, 3 + kind, 0.0, bytes});
+    a = b = nullptr;
+  }
+  ~ProfSpan() {  // not done (error path): events back to the pool
+    if (a) m->prof_pool.push_back(a);
+    if (b) m->prof_pool.push_back(b);
+  }
+};
 
 // Planar launches run gemm_pingpong_kernel (split-K below 192 tiles; measured
 // faster than the 128x128 tile at every size the sweeps produce);
@@ -502,8 +528,9 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
 
 // y: fp32 [rows][ldy] (ACT_F32) or a planar activation format
 int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
-                 int d, float eps, int fmt, hipStream_t st) {
+                 int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr) {
   if (rows <= 0) return TVR_OK;
+  ProfSpan ps(m, st);
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
     return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
   const int rows_per_block = 4;
@@ -515,6 +542,8 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   else
     hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
   TVR_HIP(hipGetLastError());
+  // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B, bf16 2 B per element)
+  ps.done(TVR_HBM_LNPRE, (double)rows * d * (4.0 + (fmt == ACT_BF16 ? 2.0 : 4.0)));
   return TVR_OK;
 }
 
@@ -613,16 +642,28 @@ GemmEpi epi_qkv_mlpin(tvr_model* m, const float* b1, float* qkv, const Acts& a) 
   return e;
 }
 
+// Algorithmic bytes of one attention launch: Q of the queried rows and K, V of
+// every row of the launch (fp32 qkv), z out in the activation format, plus the
+// fp32 hook_z copy when one is written (trace / capture).  The shared prefix
+// rows read from the trace or a leader are not counted.
+double attention_bytes(int d, int q_rows, int kv_rows, int fmt, bool zf) {
+  return ((double)q_rows * d + 2.0 * kv_rows * d) * 4.0 +
+         (double)q_rows * d * ((fmt == ACT_BF16 ? 2.0 : 4.0) + (zf ? 4.0 : 0.0));
+}
+
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
               Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m));
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, R, m->D1, d,
                       e1, st, m));
-  return launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st);
+  ProfSpan ps(m, st);
+  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf != nullptr));
+  return TVR_OK;
 }
 
 // The last layer when only each sequence's LAST row is read afterwards (patch
@@ -637,7 +678,7 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m));
   GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row (all below n_split: no GELU)
   kv.bias = w.b1 + d;
   kv.out0 = a.qkv + d;
@@ -650,7 +691,9 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e1.out_rows = d_last;
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, n_last, m->D1,
                       d, e1, st, m));
+  ProfSpan ps(m, st);
   TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf != nullptr));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
   e2.bias = w.b2;
@@ -683,17 +726,19 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
   const int d = c.d_model, V = c.d_vocab;
   for (int s = 0; s < n; s += kFinalChunk) {
     const int cn = std::min(kFinalChunk, n - s);
-    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st));
+    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m));
     float* lg = out_logits ? out_logits + (size_t)s * V : logits_ws;
     GemmEpi e{};
     e.bias = m->b_unembed;
     e.out0 = lg;
     e.ld0 = V;
     TVR_TRY(launch_gemm(EPI_BIAS, xf, d, fmt, m->wu, d, cn, V, d, e, st, m));
+    ProfSpan ps(m, st);
     hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
                        d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
                        out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
     TVR_HIP(hipGetLastError());
+    ps.done(TVR_HBM_ROW_STATS, (double)cn * V * 4.0);  // one fp32 logit row per site
   }
   return TVR_OK;
 }
@@ -916,6 +961,7 @@ int tvr_profile_read(tvr_model* m, tvr_kernel_stats* out) {
   if (!m || !out) return fail(TVR_ERR_INVALID, "tvr_profile_read: null argument");
   tvr_kernel_stats s{};
   for (auto& r : m->prof_recs) {
+    if (r.epi >= 3) continue;  // HBM-bound kernels: tvr_profile_read_hbm
     TVR_HIP(hipEventSynchronize(r.b));
     float ms = 0.f;
     TVR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
@@ -923,6 +969,23 @@ int tvr_profile_read(tvr_model* m, tvr_kernel_stats* out) {
     s.gemm_flops[r.epi] += r.flops;
     s.gemm_bytes[r.epi] += r.bytes;
     s.gemm_ms[r.epi] += ms;
+  }
+  *out = s;
+  return TVR_OK;
+}
+
+int tvr_profile_read_hbm(tvr_model* m, tvr_hbm_stats* out) {
+  if (!m || !out) return fail(TVR_ERR_INVALID, "tvr_profile_read_hbm: null argument");
+  tvr_hbm_stats s{};
+  for (auto& r : m->prof_recs) {
+    if (r.epi < 3) continue;
+    TVR_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    TVR_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    const int k = r.epi - 3;
+    s.launches[k] += 1;
+    s.ms[k] += ms;
+    s.bytes[k] += r.bytes;
   }
   *out = s;
   return TVR_OK;
@@ -1103,11 +1166,13 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
     }
     if (capture_zsum) {
       float* part = (float*)(base + o_cap);
+      ProfSpan ps(m, st);
       hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
                          zf, d, d_last, n_seq, part, d);
       hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part,
                          capture_zsum + (size_t)l * d, d);
       TVR_HIP(hipGetLastError());
+      ps.done(TVR_HBM_CAPTURE, ((double)n_seq + 1.0) * d * 4.0);  // hook_z at every last row in, [d] out
     }
     if (!(trim && l == L - 1)) TVR_TRY(run_block_out(m, l, R, a, st));
   }
@@ -1251,6 +1316,23 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     e.vec = s.vec;
     ents[k] = e;
   }
+  // algorithmic bytes of each layer's entry launch (profiling): the clean rows
+  // read and the patched rows written, the vector, and for REPLACE_HEAD the
+  // head's z rows plus its W_O slice once per distinct head
+  std::vector<double> entry_bytes(L, 0.0);
+  for (int l = 0; l < L; ++l) {
+    std::vector<char> seen(c.n_heads, 0);
+    for (int k = l > 0 ? cnt_le[l - 1] : 0; k < cnt_le[l]; ++k) {
+      const EntryDesc& e = ents[k];
+      double b = (2.0 * e.n * d + d) * 4.0;
+      if (e.kind == TVR_SITE_REPLACE_HEAD_ALLPOS) {
+        b += (double)e.n * c.d_head * 4.0;
+        if (!seen[e.head]) b += (double)d * c.d_head * 4.0;
+        seen[e.head] = 1;
+      }
+      entry_bytes[l] += b;
+    }
+  }
   std::vector<int32_t> last(n_sites), tg(n_sites), last_sorted(n_sites);
   for (int i = 0; i < n_sites; ++i) {
     last[i] = row0[i] + nrow[i] - 1;
@@ -1306,10 +1388,12 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     if (zbytes > 64 * 1024)
       TVR_HIP(hipFuncSetAttribute((const void*)entry_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)zbytes));
+    ProfSpan ps(m, st);
     hipLaunchKernelGGL(entry_kernel, dim3(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS),
                        dim3(ENTRY_THREADS), zbytes, st, d_ents + k0, snap, zsnap, w2, m->K2, vectors,
                        a.resid, d, c.d_head);
     TVR_HIP(hipGetLastError());
+    ps.done(TVR_HBM_ENTRY, entry_bytes[l]);
     return TVR_OK;
   };
 

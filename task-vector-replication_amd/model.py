@@ -272,7 +272,7 @@ class Model(TokenizerMixin):
 
     # ------------------------------------------------------------ profiling
     def profile(self, on: bool) -> None:
-        """Enable/disable HIP-event timing of every GEMM launch (resets totals)."""
+        """Enable/disable HIP-event timing of every GEMM and HBM-bound kernel launch (resets totals)."""
         _lib.check(self._lib.tvr_profile_enable(self._h, 1 if on else 0), "tvr_profile_enable")
 
     def profile_stats(self) -> dict:
@@ -282,6 +282,16 @@ class Model(TokenizerMixin):
                       "bytes": st.gemm_bytes[i]} for i, name in enumerate(_lib.GEMM_VARIANTS)}
         per["all"] = {k: sum(v[k] for v in per.values()) for k in ("launches", "flops", "ms", "bytes")}
         return per
+
+    def profile_hbm_stats(self) -> dict:
+        """The HBM-bound kernels timed since ``profile(True)``: launches, summed
+        ms, algorithmic bytes and achieved GB/s per kind (include/tvr.h
+        tvr_hbm_kind)."""
+        st = _lib.CHbmStats()
+        _lib.check(self._lib.tvr_profile_read_hbm(self._h, ctypes.byref(st)), "tvr_profile_read_hbm")
+        return {name: {"launches": st.launches[i], "ms": st.ms[i], "bytes": st.bytes[i],
+                       "gbps": st.bytes[i] / (st.ms[i] * 1e-3) / 1e9 if st.ms[i] > 0 else None}
+                for i, name in enumerate(_lib.HBM_KINDS)}
 
     # ------------------------------------------------- TL-style conveniences
     def _as_ids(self, tokens) -> List[int]:

@@ -631,3 +631,27 @@ def test_sweeps_are_deterministic(tiny_model):
         cie = tvr_amd.calculate_average_causal_indirect_effect(mean, prompts, answers, model=tiny_model)
         outs.append((mean.cpu(), cie.cpu()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_profile_counts_gemm_and_hbm_kernels(tiny_model):
+    """tvr_profile_read / tvr_profile_read_hbm: every kernel family of a CIE
+    sweep and of an extraction is timed, with positive algorithmic bytes."""
+    task = tvr_amd.tasks.letter_to_caps
+    random.seed(5)
+    tiny_model.profile(True)
+    mean = tvr_amd.generate_mean_activation(task, ARROW, ",", model=tiny_model, num_contexts=16, len_contexts=4)
+    ex = tiny_model.profile_hbm_stats()
+    tiny_model.profile(True)  # reset
+    random.seed(6)
+    prompts, answers = tvr_amd.generate_shuffled_prompts(task, tiny_model, 2, 4, ARROW)
+    tvr_amd.calculate_average_causal_indirect_effect(mean, prompts, answers, model=tiny_model)
+    gemm = tiny_model.profile_stats()
+    hbm = tiny_model.profile_hbm_stats()
+    tiny_model.profile(False)
+    L = tiny_model.cfg.n_layers
+    assert ex["capture"]["launches"] == L and ex["capture"]["bytes"] > 0 and ex["capture"]["ms"] > 0
+    assert gemm["all"]["launches"] > 0 and gemm["all"]["flops"] > 0
+    for k in ("entry", "lnpre", "attention", "row_stats"):
+        assert hbm[k]["launches"] > 0 and hbm[k]["bytes"] > 0 and hbm[k]["gbps"] > 0, k
+    assert hbm["capture"]["launches"] == 0
+    assert hbm["entry"]["launches"] <= L  # one injection launch per entry layer
