@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 LIB_NAME = "libtvr.so"
-LIB_PATH = Path(__file__).resolve().parent / LIB_NAME
+# TVR_LIB: another in-tree build of the engine (same-box A/B of two builds)
+LIB_PATH = Path(os.environ["TVR_LIB"]).resolve() if os.environ.get("TVR_LIB") else Path(__file__).resolve().parent / LIB_NAME
 
 # enum tvr_status
 TVR_OK = 0

@@ -90,6 +90,18 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     const int qi = min(q0 + li, sd.n - 1);
     float qf[CH];
     load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
+    // one key tile (T <= 16, the C3 sweeps): V's fragments are loaded with Q and
+    // K, so the wave pays one global-memory latency instead of two
+    constexpr int VP = NKT == 1 ? 4 : 1, VPD = NKT == 1 ? NDT : 1;
+    float vpre[VP][VPD];
+    if constexpr (NKT == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* vr = row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
+      }
+    }
 
     f4 st[MAXKT];
 #pragma unroll
@@ -152,10 +164,16 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
       if (kt < nkt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+          if constexpr (NKT == 1) {
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt)
-            zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+            for (int dt = 0; dt < NDT; ++dt)
+              zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vpre[r][dt], st[kt][r], zt[dt], 0, 0, 0);
+          } else {
+            const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt)
+              zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);
