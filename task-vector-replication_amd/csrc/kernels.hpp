@@ -315,7 +315,7 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
 // Capture + mean-over-prompts reduction, z form (mean_p result =
 // (mean_p z) @ W_O).  Deterministic two-pass: partial[g][c] = sum over rows
 // g, g+G, ...; then zsum[c] += sum_g partial[g][c].
-constexpr int CAP_GROUPS = 64;
+constexpr int CAP_GROUPS = 128;  // row groups of the partial pass (fixed-order sums: deterministic)
 __global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
                                        const int32_t* __restrict__ rows, int n,
                                        float* __restrict__ partial, int d) {
@@ -323,7 +323,17 @@ __global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
   const int g = blockIdx.y;
   if (c4 * 4 >= d) return;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = g; i < n; i += CAP_GROUPS) {
+  int i = g;
+  for (; i + 3 * CAP_GROUPS < n; i += 4 * CAP_GROUPS) {  // four rows' loads in flight, summed in row order
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ((const float4*)(z + (size_t)rows[i + u * CAP_GROUPS] * ldz))[c4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+    }
+  }
+  for (; i < n; i += CAP_GROUPS) {
     const float4 v = ((const float4*)(z + (size_t)rows[i] * ldz))[c4];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
@@ -358,65 +368,111 @@ __global__ void project_heads_kernel(const float* __restrict__ zsum,
 constexpr int STATS_THREADS = 256;
 constexpr int STATS_MAX_K = 16;
 
+// One pass over the row (float4 loads when the row is 16-B aligned): each
+// thread keeps an online (max, sum of exp) pair and its running argmax; the
+// block combines them in a fixed order (deterministic).  Top-k rounds after
+// the first rescan the row (L2-resident) with the chosen ids excluded.
+__device__ __forceinline__ void stats_merge(float& m, float& s, float om, float os) {
+  const float nm = fmaxf(m, om);
+  s = (m == -INFINITY ? 0.f : s * expf(m - nm)) + (om == -INFINITY ? 0.f : os * expf(om - nm));
+  m = nm;
+}
+__device__ __forceinline__ void argmax_merge(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+
 __global__ void __launch_bounds__(STATS_THREADS)
 row_stats_kernel(const float* __restrict__ logits, int ldl, int V,
                  const int32_t* __restrict__ targets, float* __restrict__ out_prob,
                  int32_t* __restrict__ out_topk, int topk) {
   __shared__ float s_val[STATS_THREADS / 64];
   __shared__ int s_idx[STATS_THREADS / 64];
-  __shared__ float s_red[STATS_THREADS / 64];
+  __shared__ float s_m[STATS_THREADS / 64], s_s[STATS_THREADS / 64];
   __shared__ int s_sel[STATS_MAX_K];
   const int r = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const float* x = logits + (size_t)r * ldl;
 
-  // block max
-  float mx = -INFINITY;
-  for (int v = t; v < V; v += STATS_THREADS) mx = fmaxf(mx, x[v]);
-  mx = wave_max(mx);
-  if (lane == 0) s_red[wave] = mx;
-  __syncthreads();
-  mx = s_red[0];
-  for (int w = 1; w < STATS_THREADS / 64; ++w) mx = fmaxf(mx, s_red[w]);
-  __syncthreads();
-  // sum of exp
-  float se = 0.f;
-  for (int v = t; v < V; v += STATS_THREADS) se += expf(x[v] - mx);
-  se = wave_sum(se);
-  if (lane == 0) s_red[wave] = se;
+  float m = -INFINITY, se = 0.f, bv = -INFINITY;
+  int bi = 0x7fffffff;
+  const bool vec = (((uintptr_t)x) & 15) == 0;
+  const int V4 = vec ? V >> 2 : 0;
+  for (int q = t; q < V4; q += STATS_THREADS) {
+    const float4 v = ((const float4*)x)[q];
+    const float m4 = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+    if (m4 > m) {
+      se = (m == -INFINITY ? 0.f : se * expf(m - m4));
+      m = m4;
+    }
+    se += (expf(v.x - m) + expf(v.y - m)) + (expf(v.z - m) + expf(v.w - m));
+    argmax_merge(bv, bi, v.x, 4 * q);
+    argmax_merge(bv, bi, v.y, 4 * q + 1);
+    argmax_merge(bv, bi, v.z, 4 * q + 2);
+    argmax_merge(bv, bi, v.w, 4 * q + 3);
+  }
+  for (int v = 4 * V4 + t; v < V; v += STATS_THREADS) {  // tail (or the whole row, unaligned)
+    const float xv = x[v];
+    if (xv > m) {
+      se = (m == -INFINITY ? 0.f : se * expf(m - xv));
+      m = xv;
+    }
+    se += expf(xv - m);
+    argmax_merge(bv, bi, xv, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(se, o, 64);
+    stats_merge(m, se, om, os);
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    argmax_merge(bv, bi, ov, oi);
+  }
+  if (lane == 0) {
+    s_m[wave] = m;
+    s_s[wave] = se;
+    s_val[wave] = bv;
+    s_idx[wave] = bi;
+  }
   __syncthreads();
   if (t == 0) {
-    float tot = 0.f;
-    for (int w = 0; w < STATS_THREADS / 64; ++w) tot += s_red[w];
+    float fm = s_m[0], fs = s_s[0], fv = s_val[0];
+    int fi = s_idx[0];
+    for (int w = 1; w < STATS_THREADS / 64; ++w) {
+      stats_merge(fm, fs, s_m[w], s_s[w]);
+      argmax_merge(fv, fi, s_val[w], s_idx[w]);
+    }
     if (out_prob) {
       const int tg = targets ? targets[r] : -1;
-      out_prob[r] = (tg >= 0 && tg < V) ? expf(x[tg] - mx) / tot : 0.f;
+      out_prob[r] = (tg >= 0 && tg < V) ? expf(x[tg] - fm) / fs : 0.f;
+    }
+    if (out_topk && topk > 0) {
+      s_sel[0] = fi;
+      out_topk[(size_t)r * topk] = fi;
     }
   }
-  if (!out_topk || topk <= 0) return;
-  // top-k: k rounds of (value desc, index asc) block argmax with exclusion
-  for (int j = 0; j < topk; ++j) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
+  if (!out_topk || topk <= 1) return;
+  __syncthreads();
+  // top-k rounds 1..k-1: (value desc, index asc) block argmax with exclusion
+  for (int j = 1; j < topk; ++j) {
+    bv = -INFINITY;
+    bi = 0x7fffffff;
     for (int v = t; v < V; v += STATS_THREADS) {
       bool taken = false;
       for (int q = 0; q < j; ++q) taken |= (s_sel[q] == v);
       if (taken) continue;
-      const float xv = x[v];
-      if (xv > bv || (xv == bv && v < bi)) { bv = xv; bi = v; }
+      argmax_merge(bv, bi, x[v], v);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float ov = __shfl_xor(bv, o, 64);
       const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      argmax_merge(bv, bi, ov, oi);
     }
     if (lane == 0) { s_val[wave] = bv; s_idx[wave] = bi; }
     __syncthreads();
     if (t == 0) {
       float fv = s_val[0];
       int fi = s_idx[0];
-      for (int w = 1; w < STATS_THREADS / 64; ++w)
-        if (s_val[w] > fv || (s_val[w] == fv && s_idx[w] < fi)) { fv = s_val[w]; fi = s_idx[w]; }
+      for (int w = 1; w < STATS_THREADS / 64; ++w) argmax_merge(fv, fi, s_val[w], s_idx[w]);
       s_sel[j] = fi;
       out_topk[(size_t)r * topk + j] = fi;
     }
