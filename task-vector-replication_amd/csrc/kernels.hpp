@@ -76,6 +76,7 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
 // One wave per row; rows optionally gathered through `row_idx`.  FMT: y is
 // fp32 (ACT_F32) or a planar activation format (split.hpp; ldy counts logical
 // elements); the outputs are bounded by sqrt(d), so no range check.
+constexpr int LN_REG_F4 = 20;  // float4 per lane held in registers: d <= 5120 (Pythia-12B), d % 256 == 0
 template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
@@ -87,6 +88,40 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
   const int src = row_idx ? row_idx[r] : r;
   const float4* xr = (const float4*)(x + (size_t)src * ldx);
   const int d4 = d >> 2;
+  if (d4 % 64 == 0 && d4 <= 64 * LN_REG_F4) {  // the row in registers: one global read
+    const int nv = d4 >> 6;
+    float4 v[LN_REG_F4];
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < LN_REG_F4; ++u)
+      if (u < nv) v[u] = xr[lane + 64 * u];
+#pragma unroll
+    for (int u = 0; u < LN_REG_F4; ++u)
+      if (u < nv) s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+    const float mean = wave_sum(s) / (float)d;
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < LN_REG_F4; ++u) {
+      if (u < nv) {
+        v[u].x -= mean; v[u].y -= mean; v[u].z -= mean; v[u].w -= mean;
+        ss += (v[u].x * v[u].x + v[u].y * v[u].y) + (v[u].z * v[u].z + v[u].w * v[u].w);
+      }
+    }
+    const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
+#pragma unroll
+    for (int u = 0; u < LN_REG_F4; ++u) {
+      if (u < nv) {
+        const int c = lane + 64 * u;
+        const float4 o = make_float4(v[u].x / scale, v[u].y / scale, v[u].z / scale, v[u].w / scale);
+        if constexpr (FMT != ACT_F32) {
+          store_act4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, o.x, o.y, o.z, o.w, nullptr);
+        } else {
+          ((float4*)((float*)y + (size_t)r * ldy))[c] = o;
+        }
+      }
+    }
+    return;
+  }
   float s = 0.f;
   for (int c = lane; c < d4; c += 64) {
     const float4 v = xr[c];

@@ -197,11 +197,12 @@ def test_gemm_x2f16_range_flag():
         assert flag.item() == want, big
 
 
-def test_lnpre_matches_torch():
-    x = torch.randn(77, 2560, device="cuda") * 3 + 1
+@pytest.mark.parametrize("d", [64, 100, 768, 2560, 4096, 5120, 6144])  # register path: d % 256 == 0, d <= 5120
+def test_lnpre_matches_torch(d):
+    x = torch.randn(77, d, device="cuda") * 3 + 1
     y = torch.empty_like(x)
     lib = tvr_amd._lib.load()
-    tvr_amd._lib.check(lib.tvr_lnpre_f32(x.data_ptr(), 2560, y.data_ptr(), 2560, 77, 2560, 1e-5,
+    tvr_amd._lib.check(lib.tvr_lnpre_f32(x.data_ptr(), d, y.data_ptr(), d, 77, d, 1e-5,
                                          torch.cuda.current_stream().cuda_stream), "lnpre")
     xd = x.double()
     xd = xd - xd.mean(-1, keepdim=True)
