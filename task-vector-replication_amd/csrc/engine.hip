@@ -1319,8 +1319,8 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   // algorithmic bytes of each layer's entry launch (profiling): the clean rows
   // read and the patched rows written, the vector, and for REPLACE_HEAD the
   // head's z rows plus its W_O slice once per distinct head
-  std::vector<double> entry_bytes(L, 0.0);
-  for (int l = 0; l < L; ++l) {
+  std::vector<double> entry_bytes(L + 1, 0.0);  // entry layers 0..L (L: the final norm's input)
+  for (int l = 0; l <= L; ++l) {
     std::vector<char> seen(c.n_heads, 0);
     for (int k = l > 0 ? cnt_le[l - 1] : 0; k < cnt_le[l]; ++k) {
       const EntryDesc& e = ents[k];
