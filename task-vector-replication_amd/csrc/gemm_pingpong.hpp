@@ -75,6 +75,21 @@ template <int EPI, int FMT>
 __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (&acc)[8][4], float* L, int row0,
                                                 int col0, int Mlim, int Nlim, int wr, int wc, int lane, int t,
                                                 float acc_scale) {
+  // A thread's columns are the same in every row it stores (the row step, 512
+  // threads, is a multiple of the threads per row), so the bias is loaded once
+  // before the row loops: no global load inside them, only LDS reads and stores.
+  bool split8 = false;
+  if constexpr (EPI == EPI_SPLIT_GELU_ACT) split8 = col0 >= ep.n_split && Nlim >= 256;
+  const int c8 = (t & 31) * 8, c4 = (t & 63) * 4;
+  float b8[8];
+  f32x4 b4 = {0.f, 0.f, 0.f, 0.f};
+  if (split8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b8[k] = ep.bias ? ep.bias[col0 + c8 + k] : 0.f;
+  } else if (ep.bias && c4 < Nlim) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b4[k] = ep.bias[col0 + c4 + k];
+  }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     if (wr == p) {
@@ -87,16 +102,14 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
     }
     __syncthreads();
     const int rows = min(128, Mlim - p * 128);
-    bool split8 = false;
-    if constexpr (EPI == EPI_SPLIT_GELU_ACT) split8 = col0 >= ep.n_split && Nlim >= 256;
     if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
-      for (int it = t; it < 128 * 32; it += PP_THREADS) {
-        const int r = it >> 5, c = (it & 31) * 8;
-        if (r >= rows) continue;
-        const float* src = L + r * PP_EPI_LDR + c;
-        float v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = src[k] + (ep.bias ? ep.bias[col0 + c + k] : 0.f);
+#pragma unroll 2
+      for (int r = t >> 5; r < 128; r += PP_THREADS / 32) {
+        if (r >= rows) break;
+        const float* src = L + r * PP_EPI_LDR + c8;
+        const f32x4 x0 = *(const f32x4*)src, x1 = *(const f32x4*)(src + 4);
+        float v[8] = {x0[0] + b8[0], x0[1] + b8[1], x0[2] + b8[2], x0[3] + b8[3],
+                      x1[0] + b8[4], x1[1] + b8[5], x1[2] + b8[6], x1[3] + b8[7]};
 #pragma unroll
         for (int k = 0; k < 8; k += 2) {
           const f32x2 g = gelu_erf2(f32x2{v[k], v[k + 1]});
@@ -105,20 +118,16 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
         }
         const int m = row0 + p * 128 + r;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
-        store_act8<FMT>(ep.out1h + orow * ep.ld1h + (col0 + c - ep.n_split), ep.ps1h, v, ep.range_flag);
+        store_act8<FMT>(ep.out1h + orow * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v, ep.range_flag);
       }
-    } else {
-      for (int it = t; it < 128 * 64; it += PP_THREADS) {
-        const int r = it >> 6, c = (it & 63) * 4;
-        if (r >= rows || c >= Nlim) continue;
-        f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c);
-        if (ep.bias) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] += ep.bias[col0 + c + k];
-        }
+    } else if (c4 < Nlim) {
+#pragma unroll 4
+      for (int r = t >> 6; r < 128; r += PP_THREADS / 64) {
+        if (r >= rows) break;
+        const f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
         const int m = row0 + p * 128 + r;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
-        epi_store4<EPI, FMT>(ep, orow, col0 + c, v);
+        epi_store4<EPI, FMT>(ep, orow, col0 + c4, v);
       }
     }
     __syncthreads();
