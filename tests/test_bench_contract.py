@@ -1,0 +1,39 @@
+"""bench.py's JSON helpers on CPU: the HBM-kernel block and the PMC summary
+lookup (keyed on GEMM family and workload, so counters of another workload
+never leak into a bench line)."""
+import json
+
+import bench
+
+
+def _kinds(ms, nbytes, launches):
+    return {k: {"launches": launches, "ms": ms, "bytes": nbytes, "gbps": nbytes / (ms * 1e-3) / 1e9 if ms else None}
+            for k in ("entry", "capture", "lnpre", "attention", "row_stats")}
+
+
+def test_hbm_kernels_block():
+    hbm = _kinds(2.0, 8e9, 4)  # 4 launches, 8 GB in 2 ms -> 4000 GB/s
+    ex = _kinds(1.0, 1e9, 2)
+    out = bench.hbm_kernels(hbm, ex, steps=2)
+    assert out["peak_gbps"] == bench.HBM_PEAK_GBPS
+    for k in ("entry", "lnpre", "attention", "row_stats"):
+        row = out[k]
+        assert row["launches_per_step"] == 2.0
+        assert row["avg_launch_us"] == 500.0
+        assert row["achieved_gbps"] == 4000.0 and row["frac"] == 0.5
+    assert out["capture"]["launches"] == 2 and out["capture"]["achieved_gbps"] == 1000.0
+    json.dumps(out)
+
+
+def test_hbm_kernels_absent_kinds():
+    hbm = _kinds(0.0, 0.0, 0)
+    out = bench.hbm_kernels(hbm, None, steps=1)
+    assert all(out[k] is None for k in ("entry", "lnpre", "attention", "row_stats", "capture"))
+
+
+def test_pmc_summary_keyed_on_family_and_workload():
+    p = bench.ROOT / "profiles" / "pmc_gemm_x2f16.json"
+    d = json.loads(p.read_text())
+    pmc, src = bench.pmc_summary("x2f16", d["workload"])
+    assert pmc is not None and pmc["hbm_bytes_per_launch"] > 0 and src
+    assert bench.pmc_summary("x2f16", "another workload") == (None, None)
