@@ -171,6 +171,10 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 7>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2pp8") {  // anatomy with the epilogue's global stores skipped
+          grid = gemm_pingpong_grid(s.M, s.N);
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 8>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2pp6" || path == "x2pp6g") {  // per-block anatomy (prologue / loop / epilogue)
           grid = gemm_pingpong_grid(s.M, s.N);
           GemmEpi eg = ee;
@@ -204,7 +208,7 @@ int main(int argc, char** argv) {
                              A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
         }
       };
-      if (path == "x2pp6" || path == "x2pp6g") {  // block anatomy: medians over blocks (cycles)
+      if (path == "x2pp6" || path == "x2pp6g" || path == "x2pp8") {  // block anatomy: medians over blocks (cycles)
         for (int i = 0; i < 5; ++i) run(false);
         run(true);
         hipDeviceSynchronize();
