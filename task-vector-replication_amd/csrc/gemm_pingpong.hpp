@@ -69,6 +69,12 @@ __host__ __device__ inline void pp_tile_coords(int wg, int nbm, int nbn, int& m0
 // contiguous per row.  Rows [row0, row0 + Mlim) / columns [col0, col0 + Nlim)
 // of the output; ep's out0 / out1h / resid / out_rows / bias index globally.
 constexpr int PP_EPI_LDR = 260;                   // floats per LDS row
+#ifndef TVR_PP_NT
+#define TVR_PP_NT 1
+#endif
+// QKV + MLP-in outputs (qkv fp32, GELU planes: 72 KB per row) stored non-temporal:
+// +2 % on that GEMM (the residual / unembed outputs measured no better); A/B: -DTVR_PP_NT=0
+constexpr bool PP_NT_STORES = TVR_PP_NT;
 constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
 
 template <int EPI, int FMT, bool NOSTORE = false>
@@ -119,7 +125,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
         const int m = row0 + p * 128 + r;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
         if (!NOSTORE || v[0] == 1.2345e-30f)  // NOSTORE (diagnostic): the LDS pass and math without the stores
-          store_act8<FMT>(ep.out1h + orow * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v, ep.range_flag);
+          store_act8<FMT, PP_NT_STORES>(ep.out1h + orow * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v, ep.range_flag);
       }
     } else if (c4 < Nlim) {
 #pragma unroll 4
@@ -128,7 +134,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
         const f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
         const int m = row0 + p * 128 + r;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
-        if (!NOSTORE || v[0] == 1.2345e-30f) epi_store4<EPI, FMT>(ep, orow, col0 + c4, v);
+        if (!NOSTORE || v[0] == 1.2345e-30f)
+          epi_store4<EPI, FMT, PP_NT_STORES && EPI == EPI_SPLIT_GELU_ACT>(ep, orow, col0 + c4, v);
       }
     }
     __syncthreads();

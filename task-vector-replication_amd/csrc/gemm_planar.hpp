@@ -86,15 +86,25 @@ __device__ __forceinline__ int planar_g(int row) {
     return (row >> 1) & 7;
 }
 
+// 16-B store, optionally non-temporal (streamed past the caches: the GEMM
+// outputs are far larger than L2 / MALL and would evict the K loop's operands)
+template <bool NT>
+__device__ __forceinline__ void st16(float* p, f32x4 v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, (f32x4*)p);
+  else
+    *(f32x4*)p = v;
+}
+
 // Four consecutive output columns of one row (VEC epilogue; N, the strides
 // and n_split are multiples of 4).
-template <int EPI, int FMT>
+template <int EPI, int FMT, bool NT = false>
 __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n0, f32x4 v) {
   if constexpr (EPI == EPI_BIAS) {
-    *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v;
+    st16<NT>(ep.out0 + orow * ep.ld0 + n0, v);
   } else if constexpr (EPI == EPI_SPLIT_GELU_ACT) {
     if (n0 < ep.n_split) {  // n_split % 4 == 0: a group never straddles it
-      *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v;
+      st16<NT>(ep.out0 + orow * ep.ld0 + n0, v);
     } else {
       const f32x2 g01 = gelu_erf2(f32x2{v[0], v[1]}), g23 = gelu_erf2(f32x2{v[2], v[3]});
       store_act4<FMT>(ep.out1h + orow * ep.ld1h + (n0 - ep.n_split), ep.ps1h, g01.x, g01.y, g23.x, g23.y,
@@ -103,7 +113,7 @@ __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n
   } else {
     static_assert(EPI == EPI_RESID, "planar epilogues: bias, split-GELU (activation format), residual");
     const f32x4 rr = *(const f32x4*)(ep.resid + orow * ep.ldr + n0);
-    *(f32x4*)(ep.out0 + orow * ep.ld0 + n0) = v + rr;
+    st16<NT>(ep.out0 + orow * ep.ld0 + n0, v + rr);
   }
 }
 

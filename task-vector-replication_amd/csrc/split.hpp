@@ -69,8 +69,15 @@ __device__ __forceinline__ void store_act4(uint16_t* p, int plane, float a, floa
 }
 
 // eight consecutive elements (p 16-B aligned): one 16-B store per plane
-template <int FMT>
+template <int FMT, bool NT = false>
 __device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (&v)[8], unsigned* flag) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  auto st = [](uint16_t* q, u32x4 x) {
+    if constexpr (NT)
+      __builtin_nontemporal_store(x, (u32x4*)q);
+    else
+      *(u32x4*)q = x;
+  };
   if constexpr (FMT == ACT_X2F16) {
     unsigned lo[4], hi[4];
     float m = 0.f;
@@ -81,14 +88,14 @@ __device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (
       hi[k] = x.h1 | ((unsigned)y.h1 << 16);
       m = fmaxf(m, fmaxf(fabsf(v[2 * k]), fabsf(v[2 * k + 1])));
     }
-    *(uint4*)p = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-    *(uint4*)(p + plane) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    st(p, u32x4{lo[0], lo[1], lo[2], lo[3]});
+    st(p + plane, u32x4{hi[0], hi[1], hi[2], hi[3]});
     if (m * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
   } else {
     unsigned w[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = bf16_bits(v[2 * k]) | ((unsigned)bf16_bits(v[2 * k + 1]) << 16);
-    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+    st(p, u32x4{w[0], w[1], w[2], w[3]});
   }
 }
 
