@@ -10,18 +10,28 @@ GPU per step.  Weights are seeded synthetic Pythia-2.8B (no checkpoints
 offline), fp32 like the reference (TransformerLens default dtype).
 
 GEMMs (95 % of the step) run on the fp32-accurate two-plane fp16 split
-(``--gemm x2f16``, default: fp32 operands split into 2 power-of-two-scaled
-fp16 planes, 3 products on v_mfma_f32_32x32x16_f16, fp32 accumulation — the
-fp16 form of 3xTF32), the three-plane bf16 split (``--gemm x3bf16``: 6
-products) or ``v_mfma_f32_32x32x2_f32`` (``--gemm f32``).  Both splits measure
-at or below the fp32 MFMA GEMM's error against fp64 (tests/test_gpu_engine.py,
-profiles/gemm_split_probe_r01.jsonl).  At N=1 an ``f32_leg`` re-times the same
-sweep on the fp32 MFMA path and reports the max CIE difference between the
-two paths.
+(``--gemm x2f16``, default: every fp32 operand split into 2 power-of-two-scaled
+fp16 planes, 3 products on v_mfma_f32_16x16x32_f16, fp32 accumulation — the
+fp16 form of 3xTF32; GEMM inputs limited to |a| < 4095, checked on the device),
+the three-plane bf16 split (``--gemm x3bf16``: 6 products) or
+``v_mfma_f32_32x32x2_f32`` (``--gemm f32``).  Both splits measure at or below
+the fp32 MFMA GEMM's error against fp64 (tests/test_gpu_engine.py,
+profiles/gemm_split_probe_r01.jsonl); ``dtype`` names the emulation.  At N=1
+an ``f32_leg`` re-times the same sweep on the fp32 MFMA path and reports the
+max CIE difference between the two paths, and ``parity`` compares the engine
+with the CPU oracle on the sites the ``cpu_baseline`` leg computes.
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): weak scaling — every rank
-sweeps its own prompts; the [L, H] CIE partial sums are all-reduced once per
-step (the mean over all prompts).  value = units of all ranks / max-rank time.
+Multi-GPU (torchrun, one rank per GPU, RCCL), ``--shard``:
+* ``heads`` (default; the metric's config C3, "patch sites sharded across the
+  GPUs"): the SAME 12 prompts on every rank, each rank owns the sites with
+  head ≡ rank (mod N) in every layer (balances the staircase exactly), one
+  SUM all-reduce of the [L, H] partials per step — strong scaling, 12,288
+  units per step in total;
+* ``prompts``: every rank sweeps its own 12 prompts over all sites — weak
+  scaling, 12,288 units per GPU per step.
+value = units of all ranks / max-rank time.  The timed region runs with no
+profiling; the kernel timings of ``roofline`` / ``hbm_kernels`` come from a
+separate profiled pass of the same step.
 
 Extra JSON objects: ``roofline`` (dominant kernel = the GEMM family, achieved
 from HIP events on the engine's launch stream), ``cpu_baseline`` (the CPU
@@ -73,7 +83,9 @@ def parse():
                          "rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-sites", type=int, default=4, help="heads per sampled layer in the CPU sample")
+    ap.add_argument("--shard", default="heads", choices=("heads", "prompts"),
+                    help="N>1: heads = C3's site split (strong scaling), prompts = per-GPU prompts (weak scaling)")
+    ap.add_argument("--profile-steps", type=int, default=2, help="steps of the separate profiled pass")
     ap.add_argument("--gemm", default="x2f16", choices=("x2f16", "x3bf16", "f32", "bf16"),
                     help="matrix-core path of the GEMMs (x2f16 / x3bf16 / f32 fp32-accurate; bf16 is the "
                          "north star's bf16 configuration, not the fp32 headline)")
@@ -129,14 +141,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(args, cfg, prompts, answers, mean):
-    """The oracle (fp32 CPU, TransformerLens semantics, one batch-1 hooked
-    forward per site — scratch2.py:181-194) on prompt 0 at layers {0, L/2,
-    L-1} x ``--cpu-sites`` heads; rate = sites / wall time."""
+def cpu_baseline(args, cfg, prompts, answers, mean, model):
+    """the oracle (fp32 CPU, TransformerLens semantics, one
+    batch-1 hooked forward per site — the reference loop scratch2.py:181-194)
+    on prompt 0 at layers {0, L/2, L-1} x ALL heads, on every host core this
+    process may use; rate = sites / wall time (per-forward time extrapolates
+    linearly to the full sweep).  Also returns ``parity``: the engine's values
+    for the same sites (same prompt, mean, layers, heads) against the oracle's."""
     import tvr_amd
     from oracle.hooked_pythia import HookedPythiaOracle, OracleConfig
     from oracle import reference_experiments as R
+    from tvr_amd.experiments import causal_indirect_effect_sums
 
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
     t0 = time.time()
     sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
     oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
@@ -144,18 +162,43 @@ def cpu_baseline(args, cfg, prompts, answers, mean):
     del sd
     log(f"cpu baseline: oracle weights ready in {time.time() - t0:.1f}s")
     layers = sorted({0, cfg.n_layers // 2, cfg.n_layers - 1})
-    heads = list(range(min(args.cpu_sites, cfg.n_heads)))
+    heads = list(range(cfg.n_heads))
     mean_cpu = mean.detach().cpu()
-    threads = torch.get_num_threads()
     t0 = time.perf_counter()
-    R.calculate_average_causal_indirect_effect(mean_cpu, [prompts[0]], [[answers[0]]], oracle,
-                                               layers=layers, heads=heads)
+    cie_ref = R.calculate_average_causal_indirect_effect(mean_cpu, [prompts[0]], [[answers[0]]], oracle,
+                                                         layers=layers, heads=heads)
     dt = time.perf_counter() - t0
     n_sites = len(layers) * len(heads)
-    return {"value": n_sites / dt, "unit": "patched prompts/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle fp32 CPU (TransformerLens semantics, batch-1 hooked forward per site, "
-                       f"reference loop scratch2.py:181-194): prompt 0 (T={len(prompts[0])}), layers {layers} x "
-                       f"heads {heads} = {n_sites} sites + 1 clean forward in {dt:.1f}s on {threads} threads")}
+    out = {"value": n_sites / dt, "unit": "patched prompts/s", "cores": cores, "kind": "port",
+           "sample": (f"oracle fp32 CPU (TransformerLens semantics, batch-1 hooked forward per site, reference loop "
+                      f"scratch2.py:181-194): prompt 0 (T={len(prompts[0])}), layers {layers} x all {len(heads)} "
+                      f"heads = {n_sites} sites + 1 clean forward in {dt:.1f}s on {cores} threads "
+                      f"(torch.set_num_threads(len(os.sched_getaffinity(0))))")}
+    # parity on the same sites: engine vs oracle
+    logits_ref = oracle.forward(torch.tensor([prompts[0]]))[0, -1]
+    clean = model.forward_clean([prompts[0]], targets=[answers[0]], topk=1, return_logits=True)
+    ours = causal_indirect_effect_sums(mean, [prompts[0]], [answers[0]], model, layers=layers).cpu().double()
+    ref = cie_ref.double()
+    idx = torch.tensor(layers)
+    d_cie = (ours[idx] - ref[idx]).abs().max().item()
+    p_ref = torch.softmax(logits_ref.double(), 0)
+    parity = {"sites": n_sites, "prompt": 0, "layers": layers, "heads": "all",
+              "max_abs_cie_err": d_cie, "max_abs_cie_ref": ref[idx].abs().max().item(),
+              "max_rel_cie_err": d_cie / max(ref[idx].abs().max().item(), 1e-30),
+              "clean_logits_max_rel_err": ((clean["logits"][0].cpu().double() - logits_ref.double()).abs().max()
+                                           / logits_ref.double().abs().max()).item(),
+              "clean_prob_abs_err": abs(clean["prob"][0].item() - p_ref[answers[0]].item()),
+              "top1_equal": int(clean["topk"][0, 0]) == int(logits_ref.argmax()),
+              "tolerance": "CIE |err| <= 1e-4 max|CIE| + 1e-7, logits 1e-4 relative, top-1 identical"}
+    parity["ok"] = bool(d_cie <= 1e-4 * ref[idx].abs().max().item() + 1e-7 and
+                        parity["clean_logits_max_rel_err"] < 1e-4 and parity["top1_equal"])
+    return out, parity
+
+
+DTYPES = {"x2f16": "f32 (x2f16 emulation: fp32 operands as 2 fp16 planes, 3 MFMA products, fp32 accumulate)",
+          "x3bf16": "f32 (x3bf16 emulation: fp32 operands as 3 bf16 planes, 6 MFMA products, fp32 accumulate)",
+          "f32": "f32 (v_mfma_f32_32x32x2_f32)",
+          "bf16": "bf16 (bf16 GEMM operands, fp32 accumulate; LayerNorm / attention / softmax fp32)"}
 
 
 def main():
@@ -172,6 +215,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     import tvr_amd
+    from tvr_amd.distributed import strided_shard
     from tvr_amd.experiments import causal_indirect_effect_sums, sum_last_z
 
     cfg = tvr_amd.get_config(args.model)
@@ -189,11 +233,12 @@ def main():
         ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, pairs, "→", ",", args.extract, 6)
         sum_last_z(model, ex_prompts[:64])  # workspace sizing outside the timed extraction
         torch.cuda.synchronize()
-        model.profile(True)
         te = time.perf_counter()
         zsum = sum_last_z(model, ex_prompts)
         torch.cuda.synchronize()
         te = time.perf_counter() - te
+        model.profile(True)  # kernel timings of the capture from a separate profiled pass
+        sum_last_z(model, ex_prompts)
         hbm_ex = model.profile_hbm_stats()
         model.profile(False)
         n_ex = len(ex_prompts)
@@ -202,11 +247,19 @@ def main():
         g = torch.Generator(device=dev).manual_seed(4321)
         mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
 
-    prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
-    units_per_step = len(prompts) * cfg.n_layers * cfg.n_heads
+    shard = args.shard if world > 1 else "heads"
+    if shard == "heads":  # C3: the same prompts everywhere, sites with head = rank (mod world)
+        prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234)
+        heads = strided_shard(cfg.n_heads, rank, world)
+        units_total = len(prompts) * cfg.n_layers * cfg.n_heads
+    else:  # weak scaling: per-rank prompts, every site
+        prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
+        heads = list(range(cfg.n_heads))
+        units_total = len(prompts) * cfg.n_layers * cfg.n_heads * world
+    units_rank = len(prompts) * cfg.n_layers * len(heads)
 
     def step():
-        cie = causal_indirect_effect_sums(mean, prompts, answers, model)
+        cie = causal_indirect_effect_sums(mean, prompts, answers, model, heads=heads)
         if world > 1:
             dist.all_reduce(cie)
         return cie
@@ -216,14 +269,14 @@ def main():
             step()
             log(f"[rank {rank}] warmup step {i + 1}/{warmup}")
         if profile:
-            model.profile(True)  # HIP events around every GEMM launch of the timed region
+            model.profile(True)  # HIP events around every launch (separate pass: not the timed value)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             cie = step()
-            log(f"[rank {rank}] step {i + 1}/{steps}")  # progress (long configs); host-side only
+            log(f"[rank {rank}] {'profiled ' if profile else ''}step {i + 1}/{steps}")  # host-side progress only
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -233,19 +286,24 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item(), cie
 
-    elapsed, cie = timed(args.warmup, args.steps, True)
-    total_units = units_per_step * args.steps * world
-    value = total_units / elapsed
+    elapsed, cie = timed(args.warmup, args.steps, False)
+    value = units_total * args.steps / elapsed
 
-    # --- roofline of the dominant kernel, from the timed region's events
+    # --- roofline of the dominant kernel + HBM-bound kernels: a separate profiled pass
+    psteps = max(1, args.profile_steps)
+    el_prof, _ = timed(0, psteps, True)
     st = model.profile_stats()
     hbm = model.profile_hbm_stats()
     model.profile(False)
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
     T = len(prompts[0])
-    workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
-                f"{args.kshot}-shot, T={T}")
+    if shard == "heads" and world > 1:
+        workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/step, "
+                    f"{args.kshot}-shot, T={T}, sites h = rank (mod {world})")
+    else:
+        workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
+                    f"{args.kshot}-shot, T={T}")
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     peak = PEAKS[args.gemm]
@@ -261,6 +319,10 @@ def main():
                               "achieved_tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2),
                               "avg_launch_ms": round(v["ms"] / v["launches"], 4),
                               "share_of_gemm_time": round(v["ms"] / fam["ms"], 4)}
+    parallelism = ("single GPU" if world == 1 else
+                   f"sites sharded by head mod {world} (same {args.prompts} prompts on every GPU), weights replicated, "
+                   f"1 all-reduce of [L,H] per step" if shard == "heads" else
+                   f"prompt-sharded x{world}, weights replicated, 1 all-reduce of [L,H] per step")
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -270,14 +332,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard == "heads" else "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if args.gemm == "bf16" else "f32",
+        "dtype": DTYPES[args.gemm],
         "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
         "config": {
             "workload": workload,
-            "sites_per_step_per_gpu": units_per_step,
-            "parallelism": f"prompt-sharded x{world}, weights replicated, 1 all-reduce of [L,H] per step",
+            "sites_per_step": units_total,
+            "sites_per_step_per_gpu": units_rank,
+            "parallelism": parallelism,
+            "shard": shard,
         },
         "roofline": {
             "bound": "mfma",
@@ -286,7 +350,7 @@ def main():
             "peak": round(peak, 1),
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "flops_basis": "algorithmic fp32 2*M*N*K per launch / HIP-event launch time",
+            "flops_basis": "algorithmic fp32 2*M*N*K per launch / HIP-event launch time (separate profiled pass)",
             "peak_basis": ("fp32 MFMA dense peak" if args.gemm == "f32" else
                            f"fp16/bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {PRODUCTS[args.gemm]} products "
                            f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
@@ -294,35 +358,33 @@ def main():
             "traffic_source": traffic_src,
             "mfma_util_rocprof": (pmc.get("mfma") or {}).get("all") if pmc else None,
             "algorithmic_bytes_per_launch": round(fam["bytes"] / max(fam["launches"], 1)),
-            "launches_per_step": fam["launches"] // args.steps,
+            "launches_per_step": fam["launches"] // psteps,
             "avg_launch_gflop": round(fam["flops"] / max(fam["launches"], 1) / 1e9, 3),
             "avg_launch_ms": round(fam["ms"] / max(fam["launches"], 1), 4),
-            "gemm_share_of_step": round(fam["ms"] / (elapsed * 1e3), 4),
+            "gemm_share_of_step": round(fam["ms"] / (el_prof * 1e3), 4),
             "variants": variants,
         },
-        "hbm_kernels": hbm_kernels(hbm, hbm_ex, args.steps),
+        "hbm_kernels": hbm_kernels(hbm, hbm_ex, psteps),
         "algorithmic": {
             "gflop_per_site": round(f_alg / 1e9, 2),
-            "site_tflops": round(value / world * f_alg / 1e12, 2),
+            "site_tflops": round(value * f_alg / 1e12, 2),
             "extraction_prompts_per_s": round(n_ex / te, 1) if te else None,
         },
     }
     out["config"]["gemm"] = args.gemm
     if world == 1 and args.f32_leg and args.gemm != "f32":
         model.set_gemm("f32")
-        el32, cie32 = timed(1, max(1, min(args.steps, 2)), True)
-        st32 = model.profile_stats()["all"]
-        model.profile(False)
+        n32 = max(1, min(args.steps, 2))
+        el32, cie32 = timed(1, n32, False)
         model.set_gemm(args.gemm)
         out["f32_leg"] = {
-            "gemm": "f32", "steps": max(1, min(args.steps, 2)),
-            "value": round(units_per_step * max(1, min(args.steps, 2)) / el32, 2),
-            "gemm_tflops": round(st32["flops"] / (st32["ms"] * 1e-3) / 1e12, 2),
+            "gemm": "f32", "steps": n32,
+            "value": round(units_rank * n32 / el32, 2),
             "max_abs_cie_diff_vs_f32": float((cie - cie32).abs().max()),
             "max_abs_cie": float(cie32.abs().max()),
         }
     if rank == 0 and world == 1 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, cfg, prompts, answers, mean)
+        out["cpu_baseline"], out["parity"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -23,7 +23,12 @@
  *   - Every function returns TVR_OK (0) or a negative error code; no C++
  *     exception crosses the ABI.  tvr_last_error() explains the last failure
  *     on the calling thread.
- *   - All arithmetic is fp32 (the reference's TransformerLens default dtype).
+ *   - Numerics: LayerNorm, attention, the residual stream, the injections and
+ *     the softmax are fp32 (the reference's TransformerLens default dtype).
+ *     The GEMMs run on the matrix-core path chosen by tvr_model_set_gemm:
+ *     TVR_GEMM_F32 at tvr_model_create; the Python façade selects
+ *     TVR_GEMM_X2F16, an fp32-accurate emulation (each fp32 operand as two
+ *     fp16 planes, three fp16 MFMA products, fp32 accumulation), by default.
  */
 #ifndef TVR_H_
 #define TVR_H_

@@ -92,38 +92,62 @@ def _layer_vectors(layered_vectors: torch.Tensor, model: Model, late_binding: bo
     return v.contiguous(), lambda layer: layer
 
 
-def _injection_sweep(model: Model, seqs: List[List[int]], vectors: torch.Tensor, vec_of_layer,
-                     layers: Sequence[int], targets: Optional[List[int]], topk: int):
-    """Clean forward of ``seqs`` + one ADD_ATTN_OUT_LASTPOS site per
-    (prompt, layer).  Returns (clean outputs, patched outputs [n, len(layers)])."""
-    n = len(seqs)
-    trace = model.trace(n, sum(len(s) for s in seqs))
+def _add_site_outputs(model: Model, seqs: List[List[int]], site_seq, site_layer, site_vec, vectors: torch.Tensor,
+                      targets: Optional[List[int]], topk: int, shard=None):
+    """Clean forward of ``seqs`` + the ADD_ATTN_OUT_LASTPOS sites
+    (``hook_attn_out[0, -1] += vectors[vec]`` at ``layer``, scratch2.py:107-109)
+    of the global site list (site_seq, site_layer, site_vec).  ``shard``
+    (distributed.SiteShard) evaluates only this rank's sites and all-gathers
+    the per-site outputs, so every rank returns every site in global order.
+    Returns (clean outputs per prompt, patched outputs per site)."""
+    n_sites = len(site_seq)
+    sel = np.arange(n_sites) if shard is None else np.asarray(shard.select(n_sites), dtype=np.int64)
+    trace = model._sweep_trace(len(seqs), sum(len(s) for s in seqs))
     clean = model.forward_clean(seqs, targets=targets, topk=topk, trace=trace)
-    sites = make_sites(n * len(layers))
-    sites["seq"] = np.repeat(np.arange(n), len(layers))
-    sites["layer"] = np.tile(np.asarray(layers), n)
-    sites["kind"] = _lib.SITE_ADD_ATTN_OUT_LASTPOS
-    sites["vec"] = [vec_of_layer(l) for l in sites["layer"]]
-    if targets is not None:
-        sites["target"] = np.repeat(np.asarray(targets), len(layers))
+    dev = model.device
     patched = {}
-    for a, b in _chunks(len(sites), MAX_SITES_PER_LAUNCH):
-        out = model.patch_sweep(trace, sites[a:b], vectors, topk=topk, want_prob=targets is not None)
-        for k, v in out.items():
-            patched.setdefault(k, []).append(v)
-    patched = {k: torch.cat(v).view(n, len(layers), *v[0].shape[1:]) for k, v in patched.items()}
+    if targets is not None:
+        patched["prob"] = [torch.empty(0, device=dev)]
+    if topk:
+        patched["topk"] = [torch.empty(0, topk, dtype=torch.int32, device=dev)]
+    if len(sel):
+        patched = {k: [] for k in patched}
+        sites = make_sites(len(sel))
+        sites["kind"] = _lib.SITE_ADD_ATTN_OUT_LASTPOS
+        sites["seq"] = np.asarray(site_seq)[sel]
+        sites["layer"] = np.asarray(site_layer)[sel]
+        sites["vec"] = np.asarray(site_vec)[sel]
+        if targets is not None:
+            sites["target"] = np.asarray(targets)[sites["seq"]]
+        for a, b in _chunks(len(sites), MAX_SITES_PER_LAUNCH):
+            out = model.patch_sweep(trace, sites[a:b], vectors, topk=topk, want_prob=targets is not None)
+            for k in patched:
+                patched[k].append(out[k])
+    patched = {k: torch.cat(v) for k, v in patched.items()}
+    if shard is not None:
+        patched = {k: shard.gather(v, n_sites) for k, v in patched.items()}
     return clean, patched
 
 
-def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: Pairs, function_token: str,
-                                       model: Model = None, reference_late_binding: bool = True) -> List[float]:
-    """Per-layer top-1 accuracy of zero-shot ``[BOS, x, f]`` prompts with a
-    vector added to ``hook_attn_out[0, -1]`` at that layer."""
+def _injection_sweep(model: Model, seqs: List[List[int]], vectors: torch.Tensor, vec_of_layer,
+                     layers: Sequence[int], targets: Optional[List[int]], topk: int, shard=None):
+    """One ADD_ATTN_OUT_LASTPOS site per (prompt, layer).  Returns (clean
+    outputs, patched outputs [n, len(layers)])."""
+    n, layers = len(seqs), list(layers)
+    site_layer = np.tile(np.asarray(layers, dtype=np.int32), n)
+    clean, patched = _add_site_outputs(model, seqs, np.repeat(np.arange(n, dtype=np.int32), len(layers)), site_layer,
+                                       np.asarray([vec_of_layer(l) for l in site_layer], dtype=np.int32), vectors,
+                                       targets, topk, shard)
+    return clean, {k: v.view(n, len(layers), *v.shape[1:]) for k, v in patched.items()}
+
+
+def _zero_shot_accuracy(layered_vectors, contexts: Pairs, function_token: str, model: Model,
+                        reference_late_binding: bool, shard=None) -> List[float]:
     L = model.cfg.n_layers
     vectors, vec_of = _layer_vectors(layered_vectors, model, reference_late_binding)
     f = model.to_single_token(function_token)
     seqs = [[0, model.to_single_token(x), f] for x, _ in contexts]
-    _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, topk=1)
+    _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, 1, shard)
     top1 = patched["topk"][..., 0].cpu().tolist()
     hits = [0] * L
     for (x, y), row in zip(contexts, top1):
@@ -132,22 +156,44 @@ def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: 
     return [1.0 * h / len(contexts) for h in hits]
 
 
-def apply_layered_vectors_to_zero_shot_by_probability(layered_vectors: torch.Tensor, contexts: Pairs,
-                                                      function_token: str, model: Model = None,
-                                                      reference_late_binding: bool = True) -> torch.Tensor:
-    """Per-layer mean change of the first answer token's probability
-    (patched − clean), [n_layers] on the device."""
+def _zero_shot_dprob(layered_vectors, contexts: Pairs, function_token: str, model: Model,
+                     reference_late_binding: bool, shard=None) -> torch.Tensor:
     L = model.cfg.n_layers
     vectors, vec_of = _layer_vectors(layered_vectors, model, reference_late_binding)
     f = model.to_single_token(function_token)
     enc = model.tokenizer.encode
     seqs = [[0] + enc(x) + [f] for x, _ in contexts]
     targets = [enc(y)[0] for _, y in contexts]
-    clean, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), targets, topk=0)
+    clean, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), targets, 0, shard)
     return (patched["prob"] - clean["prob"][:, None]).sum(0) / len(contexts)
 
 
+def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: Pairs, function_token: str,
+                                       model: Model = None, reference_late_binding: bool = True) -> List[float]:
+    """Per-layer top-1 accuracy of zero-shot ``[BOS, x, f]`` prompts with a
+    vector added to ``hook_attn_out[0, -1]`` at that layer."""
+    return _zero_shot_accuracy(layered_vectors, contexts, function_token, model, reference_late_binding)
+
+
+def apply_layered_vectors_to_zero_shot_by_probability(layered_vectors: torch.Tensor, contexts: Pairs,
+                                                      function_token: str, model: Model = None,
+                                                      reference_late_binding: bool = True) -> torch.Tensor:
+    """Per-layer mean change of the first answer token's probability
+    (patched − clean), [n_layers] on the device."""
+    return _zero_shot_dprob(layered_vectors, contexts, function_token, model, reference_late_binding)
+
+
 # ------------------------------------------------------------------- a6 / a7
+def normalize_cie_inputs(model: Model, scrambled_prompts, prompt_answers):
+    """The reference's prompt / answer forms → token-id prompts (BOS
+    prepended to strings by ``to_tokens``, scratch2.py:182) and first answer
+    token ids (``[answer][0]``, scratch2.py:184,192: B3)."""
+    prompts = [model.to_tokens(p)[0].tolist() if isinstance(p, str) else [int(x) for x in p]
+               for p in scrambled_prompts]
+    answers = [int(a[0]) if isinstance(a, (list, tuple)) else int(a) for a in prompt_answers]
+    return prompts, answers
+
+
 def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Sequence[Sequence[int]],
                                 answers: Sequence[int], model: Model,
                                 layers: Optional[Sequence[int]] = None,
@@ -170,7 +216,7 @@ def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Se
         seqs = [list(map(int, p)) for p in prompts[a:b]]
         tg = [int(t) for t in answers[a:b]]
         n = len(seqs)
-        trace = model.trace(n, sum(len(s) for s in seqs))
+        trace = model._sweep_trace(n, sum(len(s) for s in seqs))
         p0 = model.forward_clean(seqs, targets=tg, trace=trace)["prob"]
         sites = make_sites(n * per_prompt)
         sites["seq"] = np.repeat(np.arange(n, dtype=np.int32), per_prompt)
@@ -196,8 +242,7 @@ def calculate_average_causal_indirect_effect(mean_head_activations: torch.Tensor
         raise ValueError("Mean head activations must be of shape (n_layers, n_heads, d_model)")
     if len(scrambled_prompts) != len(prompt_answers):
         raise ValueError("Prompt answers must be of the same length as scrambled prompts")
-    prompts = [model.to_tokens(p)[0].tolist() if isinstance(p, str) else list(p) for p in scrambled_prompts]
-    answers = [a[0] if isinstance(a, (list, tuple)) else int(a) for a in prompt_answers]
+    prompts, answers = normalize_cie_inputs(model, scrambled_prompts, prompt_answers)
     return causal_indirect_effect_sums(mean_head_activations, prompts, answers, model) / len(prompts)
 
 
@@ -271,7 +316,7 @@ def test_component_hypothesis(contexts: Pairs, function_token: str, model: Model
             seqs.append(icl_single_token(model, demos, dummy, function_token, None))
             answers.append(query[1])
         n = len(answers)
-        trace = model.trace(3 * n, sum(len(s) for s in seqs))
+        trace = model._sweep_trace(3 * n, sum(len(s) for s in seqs))
         top = model.forward_clean(seqs, topk=1, trace=trace)["topk"][:, 0].cpu().view(n, 3).tolist()
         sites = make_sites(n * L)
         T = np.asarray([len(seqs[3 * i + 2]) for i in range(n)], dtype=np.int32)
@@ -312,7 +357,7 @@ def substitute_task(taskA: Pairs, taskB: Pairs, layer: int, function_token: str 
         seqs.append(icl_single_token(model, ctx_b, q, function_token, None))
         ans.append((mixed[len_contexts][1], mixed[len_contexts][2]))
     n = num_contexts
-    trace = model.trace(2 * n, sum(len(s) for s in seqs))
+    trace = model._sweep_trace(2 * n, sum(len(s) for s in seqs))
     top = model.forward_clean(seqs, topk=1, trace=trace)["topk"][:, 0].cpu().view(n, 2).tolist()
     sites = make_sites(2 * n)
     T = np.asarray([len(s) for s in seqs], dtype=np.int32)
@@ -332,26 +377,18 @@ def substitute_task(taskA: Pairs, taskB: Pairs, layer: int, function_token: str 
 
 # ------------------------------------------------------- batched FV evaluation
 def _fv_sites_topk(model: Model, contexts: Pairs, vectors: torch.Tensor, layer_vec: Sequence[Tuple[int, int]],
-                   topk: int):
+                   topk: int, shard=None):
     """Top-k hits of every (prompt, (layer, vector)) pair in ONE sweep:
     prompts ``x + ":"``, vector added to hook_attn_out[0, -1] at the layer
     (scratch2.py:306-314 semantics).  Returns hits [len(layer_vec)]."""
     seqs = [model.to_tokens(x + ":")[0].tolist() for x, _ in contexts]
     firsts = [model.to_string(model.tokenizer.encode(y)[0]) for _, y in contexts]
     n, m = len(seqs), len(layer_vec)
-    trace = model.trace(n, sum(len(s) for s in seqs))
-    model.forward_clean(seqs, trace=trace)
     lv = np.asarray(layer_vec, dtype=np.int32).reshape(m, 2)
-    sites = make_sites(n * m)
-    sites["kind"] = _lib.SITE_ADD_ATTN_OUT_LASTPOS
-    sites["seq"] = np.repeat(np.arange(n), m)
-    sites["layer"] = np.tile(lv[:, 0], n)
-    sites["vec"] = np.tile(lv[:, 1], n)
     vecs = vectors.to(model.device, torch.float32).reshape(-1, model.cfg.d_model).contiguous()
-    tops = []
-    for a, b in _chunks(len(sites), MAX_SITES_PER_LAUNCH):
-        tops.append(model.patch_sweep(trace, sites[a:b], vecs, topk=topk, want_prob=False)["topk"])
-    top = torch.cat(tops).view(n, m, topk).cpu().tolist()
+    _, patched = _add_site_outputs(model, seqs, np.repeat(np.arange(n, dtype=np.int32), m), np.tile(lv[:, 0], n),
+                                   np.tile(lv[:, 1], n), vecs, None, topk, shard)
+    top = patched["topk"].view(n, m, topk).cpu().tolist()
     hits = np.zeros(m, dtype=np.int64)
     for i, first in enumerate(firsts):
         for j in range(m):
@@ -360,32 +397,39 @@ def _fv_sites_topk(model: Model, contexts: Pairs, vectors: torch.Tensor, layer_v
 
 
 def check_accuracy_of_added_task_vector_by_layer(task_vector: torch.Tensor, contexts: Pairs, topk: int = 5,
-                                                 model: Model = None) -> List[float]:
-    """``check_accuracy_of_added_task_vector`` at every layer (one sweep)."""
+                                                 model: Model = None, shard=None) -> List[float]:
+    """``check_accuracy_of_added_task_vector`` at every layer (one sweep;
+    ``shard``: distributed.SiteShard, sites round-robin over ranks)."""
     L = model.cfg.n_layers
-    hits = _fv_sites_topk(model, contexts, task_vector.reshape(1, -1), [(l, 0) for l in range(L)], topk)
+    hits = _fv_sites_topk(model, contexts, task_vector.reshape(1, -1), [(l, 0) for l in range(L)], topk, shard)
     return [float(h) / len(contexts) for h in hits]
 
 
 def function_vector_head_count_grid(mean_head_activations: torch.Tensor, causal_indirect_effects: torch.Tensor,
                                     contexts: Pairs, model: Model = None, heads_per_batch: int = 2,
-                                    number_of_batches: int = 64, topk: int = 5) -> torch.Tensor:
+                                    number_of_batches: int = 64, topk: int = 5, shard=None) -> torch.Tensor:
     """The FV head-count grid of scratch2.py:411-425 as ONE batched sweep:
     accuracy[i, j] of the function vector made of the top (j+1)*heads_per_batch
-    heads of layers <= i, added at layer i; entries the reference skips
-    ((j+1)*k >= (i+1)*n_heads) stay 0.  [n_layers, number_of_batches]."""
+    heads of layers <= i, added at layer i.  Where the reference skips the
+    assembly ((j+1)*k >= (i+1)*n_heads, :416) its ``task_vectors[i, j]`` stays
+    the zero vector it was created as (:413) and the accuracy loop (:420-424)
+    still evaluates it: those cells are the zero vector added at layer i, i.e.
+    layer i's zero-shot top-k accuracy.  [n_layers, number_of_batches]."""
     L, H = model.cfg.n_layers, model.cfg.n_heads
-    vecs, cells = [], []
+    d = mean_head_activations.shape[-1]
+    vecs = [torch.zeros(d, dtype=torch.float32, device=model.device)]  # vector 0: the skipped cells
+    cells = []
     for i in range(L):
         for j in range(number_of_batches):
             k = (j + 1) * heads_per_batch
             if k < (i + 1) * H:
-                vecs.append(assemble_task_vector(mean_head_activations, causal_indirect_effects, i, k))
-                cells.append((i, j))
+                vecs.append(assemble_task_vector(mean_head_activations, causal_indirect_effects, i, k)
+                            .to(model.device, torch.float32))
+                cells.append((i, j, len(vecs) - 1))
+            else:
+                cells.append((i, j, 0))
+    hits = _fv_sites_topk(model, contexts, torch.stack(vecs), [(i, v) for i, _, v in cells], topk, shard)
     acc = torch.zeros(L, number_of_batches)
-    if not cells:
-        return acc
-    hits = _fv_sites_topk(model, contexts, torch.stack(vecs), [(i, v) for v, (i, _) in enumerate(cells)], topk)
-    for (i, j), h in zip(cells, hits):
+    for (i, j, _), h in zip(cells, hits):
         acc[i, j] = float(h) / len(contexts)
     return acc

@@ -24,7 +24,8 @@ import torch
 from . import _lib
 from .config import CConfig, PythiaConfig, get_config
 from .tokenizer import HFTokenizer, SyntheticTokenizer, TokenizerMixin
-from .weights import EngineWeights, load_hf_safetensors, process_to_engine, synth_engine_weights
+from .weights import (EngineWeights, config_from_hf_json, load_hf_safetensors, process_to_engine,
+                      synth_engine_weights)
 
 SITE_DTYPE = np.dtype([(f, np.int32) for f in _lib.SITE_FIELDS])
 
@@ -118,12 +119,21 @@ class Model(TokenizerMixin):
                         cfg: Optional[PythiaConfig] = None, gemm: str = DEFAULT_GEMM) -> "Model":
         """``HookedTransformer.from_pretrained`` without a network: the named
         Pythia shape with seeded synthetic weights (generated on the device), or
-        a local HF-layout safetensors ``checkpoint``.  ``gemm`` picks the
-        matrix-core path (see :meth:`set_gemm`)."""
-        cfg = cfg if cfg is not None else get_config(name)
+        a local HF-layout safetensors ``checkpoint`` (file, or directory with
+        model.safetensors / sharded index; its config.json, when present,
+        supplies the shape for names this module does not know).  ``gemm``
+        picks the matrix-core path (see :meth:`set_gemm`)."""
+        import os
+        if cfg is None:
+            try:
+                cfg = get_config(name)
+            except ValueError:
+                if not (checkpoint and os.path.isdir(checkpoint)):
+                    raise
+                cfg = config_from_hf_json(checkpoint)
         dev = torch.device(device)
         if checkpoint:
-            w = process_to_engine(cfg, load_hf_safetensors(checkpoint), device=dev, free_source=True)
+            w = process_to_engine(cfg, load_hf_safetensors(checkpoint, cfg), device=dev, free_source=True)
         else:
             w = synth_engine_weights(cfg, seed=seed, device=dev, std=std, ln_std=ln_std)
         tok = HFTokenizer(tokenizer_path) if tokenizer_path else None
@@ -171,7 +181,12 @@ class Model(TokenizerMixin):
             _lib.check(self._lib.tvr_model_range_status(self._h, self._stream()), what)
 
     def trace(self, n_seqs: int, n_tokens: int) -> Trace:
-        """A trace with at least this capacity (reused across calls)."""
+        """A new trace with this capacity, owned by the caller (the experiment
+        functions use a private one, so they never overwrite it)."""
+        return Trace(self, max(n_seqs, 1), max(n_tokens, 1))
+
+    def _sweep_trace(self, n_seqs: int, n_tokens: int) -> Trace:
+        """The experiment functions' scratch trace (grown on demand, reused)."""
         t = self._trace_cache
         if t is None or t.max_seqs < n_seqs or t.max_tokens < n_tokens:
             self._trace_cache = None

@@ -93,21 +93,28 @@ class SyntheticTokenizer:
 
 
 class HFTokenizer:
-    """Wraps a local ``tokenizer.json`` (HF ``tokenizers``) with the same API."""
+    """Wraps a local ``tokenizer.json`` (HF ``tokenizers``; Pythia's is a
+    byte-level BPE with ``<|endoftext|>`` = 0) with the same API.  Decoding
+    keeps special tokens, as TransformerLens' ``to_string`` does
+    (``tokenizer.decode(..., clean_up_tokenization_spaces=False)``)."""
 
     def __init__(self, path: str):
         from tokenizers import Tokenizer
-        self._tok = Tokenizer.from_file(path)
+        self._tok = Tokenizer.from_file(str(path))
         self.vocab_size = self._tok.get_vocab_size()
+        bos = self._tok.token_to_id(BOS_TEXT)
+        if bos is not None and bos != BOS_ID:
+            raise ValueError(f"{path}: {BOS_TEXT} is id {bos}; the reference hard-codes BOS = {BOS_ID} "
+                             "(scratch2.py:53,121,142)")
 
     def encode(self, text: str) -> List[int]:
         return self._tok.encode(text, add_special_tokens=False).ids
 
     def decode_one(self, tid: int) -> str:
-        return self._tok.decode([int(tid)])
+        return self._tok.decode([int(tid)], skip_special_tokens=False)
 
     def decode(self, ids: Iterable[int]) -> str:
-        return self._tok.decode([int(i) for i in ids])
+        return self._tok.decode([int(i) for i in ids], skip_special_tokens=False)
 
 
 TokenInput = Union[int, Sequence[int], "torch.Tensor"]  # noqa: F821

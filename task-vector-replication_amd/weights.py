@@ -81,11 +81,76 @@ def synth_hf_state_dict(cfg: PythiaConfig, seed: int = 0, device="cpu", std: flo
             for n, s in hf_param_shapes(cfg).items()}
 
 
-def load_hf_safetensors(path: str, device="cpu") -> HFStateDict:
-    """Load a local HF GPT-NeoX checkpoint (safetensors, no code execution)."""
+# Non-parameter entries real GPT-NeoX checkpoints carry per layer (buffers the
+# engine recomputes: causal mask, its fill value, rotary inverse frequencies).
+HF_BUFFER_SUFFIXES = ("attention.bias", "attention.masked_bias", "attention.rotary_emb.inv_freq")
+HF_ALIASES = {"lm_head.weight": "embed_out.weight"}
+
+
+def _checkpoint_files(path) -> List[str]:
+    """A .safetensors file, or a directory holding model.safetensors or the
+    shards listed by model.safetensors.index.json."""
+    import json
+    import os
+    if os.path.isdir(path):
+        index = os.path.join(path, "model.safetensors.index.json")
+        if os.path.exists(index):
+            with open(index) as f:
+                shards = sorted(set(json.load(f)["weight_map"].values()))
+            return [os.path.join(path, s) for s in shards]
+        single = os.path.join(path, "model.safetensors")
+        if os.path.exists(single):
+            return [single]
+        raise FileNotFoundError(f"{path}: no model.safetensors or model.safetensors.index.json")
+    return [str(path)]
+
+
+def load_hf_safetensors(path, cfg: Optional[PythiaConfig] = None, device="cpu") -> HFStateDict:
+    """Load a local HF GPT-NeoX checkpoint (``GPTNeoXForCausalLM`` layout,
+    safetensors only: no code execution), the offline replacement of the
+    by-name fetch at scratch.py:26 / scratch2.py:26.  ``path`` is a file or a
+    directory (single file or sharded with an index).  Buffers are dropped
+    (``attention.bias`` / ``masked_bias`` / ``rotary_emb.inv_freq``), the
+    ``lm_head.weight`` alias is mapped to ``embed_out.weight``, fp16 / bf16
+    tensors become fp32.  With ``cfg`` the key set and every shape are checked
+    against ``hf_param_shapes(cfg)`` (ValueError naming what is missing,
+    unexpected or mis-shaped)."""
     from safetensors.torch import load_file
-    sd = load_file(path, device=str(device))
-    return {k: v.float() for k, v in sd.items()}
+    sd: HFStateDict = {}
+    for f in _checkpoint_files(path):
+        for k, v in load_file(f, device=str(device)).items():
+            if k.endswith(HF_BUFFER_SUFFIXES):
+                continue
+            sd[HF_ALIASES.get(k, k)] = v.float()
+    if cfg is not None:
+        want = hf_param_shapes(cfg)
+        missing = sorted(set(want) - set(sd))
+        extra = sorted(set(sd) - set(want))
+        bad = sorted(k for k in set(want) & set(sd) if tuple(sd[k].shape) != tuple(want[k]))
+        if missing or extra or bad:
+            raise ValueError(f"{path}: checkpoint does not match {cfg.name} "
+                             f"(missing {missing[:6]}{'...' if len(missing) > 6 else ''}, "
+                             f"unexpected {extra[:6]}, wrong shape {bad[:6]})")
+    return sd
+
+
+def config_from_hf_json(path) -> PythiaConfig:
+    """A ``PythiaConfig`` from an HF GPT-NeoX ``config.json`` (a checkpoint
+    directory or the file).  The engine implements Pythia's block only:
+    parallel residual, rotary, exact-erf GELU."""
+    import json
+    import os
+    f = os.path.join(path, "config.json") if os.path.isdir(path) else str(path)
+    with open(f) as fh:
+        c = json.load(fh)
+    if c.get("model_type", "gpt_neox") != "gpt_neox" or not c.get("use_parallel_residual", True):
+        raise ValueError(f"{f}: only GPT-NeoX with the parallel residual (Pythia) is supported")
+    if c.get("hidden_act", "gelu") != "gelu":
+        raise ValueError(f"{f}: hidden_act {c.get('hidden_act')!r} (Pythia uses exact-erf gelu)")
+    return PythiaConfig(n_layers=c["num_hidden_layers"], d_model=c["hidden_size"], n_heads=c["num_attention_heads"],
+                        d_mlp=c["intermediate_size"], d_vocab=c["vocab_size"], rotary_pct=c.get("rotary_pct", 0.25),
+                        n_ctx=c.get("max_position_embeddings", 2048), ln_eps=c.get("layer_norm_eps", 1e-5),
+                        rotary_base=float(c.get("rotary_emb_base", 10000)), name=c.get("_name_or_path", "checkpoint"))
 
 
 @dataclass

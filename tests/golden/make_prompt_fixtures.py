@@ -70,14 +70,26 @@ def load_reference_functions(model):
 
 def main():
     import tvr_amd
-    tok = tvr_amd.tokenizer.SyntheticTokenizer(512)
+    cases = []
+    make_cases(tvr_amd.tokenizer.SyntheticTokenizer(512), None, cases)
+    # the same functions on a real byte-level BPE vocabulary (tests/golden/make_tokenizer.py)
+    make_cases(tvr_amd.tokenizer.HFTokenizer(str(Path(__file__).resolve().parent / "tokenizer.json")), "hf", cases)
+    OUT.write_text(json.dumps({"generator": "tests/golden/make_prompt_fixtures.py", "vocab": 512,
+                               "cases": cases}, indent=1) + "\n")
+    print(f"wrote {len(cases)} cases to {OUT}")
+
+
+def make_cases(tok, tok_name, cases):
+    import tvr_amd
     model = StubModel(tok)
     ref = load_reference_functions(model)
     T = tvr_amd.tasks
-    cases = []
 
     def case(fn, seed, args, kwargs, out):
-        cases.append({"fn": fn, "seed": seed, "args": args, "kwargs": kwargs, "out": out})
+        c = {"fn": fn, "seed": seed, "args": args, "kwargs": kwargs, "out": out}
+        if tok_name:
+            c["tokenizer"] = tok_name
+        cases.append(c)
 
     for seed, task, k, sep in [(0, "letter_to_caps", 4, None), (1, "low_to_caps", 6, ","), (2, "fruit_to_color", 3, "|"),
                                (3, "following_number", 5, None), (4, "state_to_capital", 5, ",")]:
@@ -86,7 +98,8 @@ def main():
         pool = pairs.copy()
         random.shuffle(pool)
         demos, q = pool[:k], pool[k][0]
-        if task in ("fruit_to_color", "state_to_capital"):
+        one = all(len(tok.encode(s)) == 1 for s in [x for p in demos for x in p] + [q, T.ARROW] + ([sep] if sep else []))
+        if task in ("fruit_to_color", "state_to_capital") or not one:
             out = ref["mix_multitoken_contexts_and_query"](demos, q, T.ARROW, sep, model)
             case("mix_multitoken_contexts_and_query", seed, [demos, q, T.ARROW, sep], {}, out)
         else:
@@ -107,9 +120,6 @@ def main():
     case("assemble_end_list_tasks", 21, [4, 3, "|"], {}, [lists, None])
     case("construct_context", None, [["a", "A"], T.ARROW], {}, ref["construct_context"](("a", "A"), T.ARROW))
     case("construct_query", None, [["b", "B"], ":"], {}, list(ref["construct_query"](("b", "B"), ":")))
-    OUT.write_text(json.dumps({"generator": "tests/golden/make_prompt_fixtures.py", "vocab": 512,
-                               "cases": cases}, indent=1) + "\n")
-    print(f"wrote {len(cases)} cases to {OUT}")
 
 
 if __name__ == "__main__":

@@ -47,9 +47,8 @@ def _worker(rank, world, port, q):
         # prompt-sharded extraction with a stand-in "Σ z" and projection
         vecs = torch.randn(10, 3, 4, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
         ids = list(range(10))
-        mean_x = D.sharded_mean_activation(ids, lambda ps: vecs[list(ps)].sum(0) if ps else torch.zeros(3, 4,
-                                                                                                   dtype=torch.float64),
-                                           lambda z: z * 2)
+        mean_x = D.sharded_mean_activation(ids, lambda ps: vecs[list(ps)].sum(0), lambda z: z * 2,
+                                           lambda: torch.zeros(3, 4, dtype=torch.float64))
         q.put((rank, cie, mean_x, D.strided_shard(cfg.n_heads, rank, world),
                D.contiguous_shard(10, rank, world)))
     finally:
@@ -89,3 +88,121 @@ def test_sharded_sweeps_match_single_process(world):
         items_seen += list(range(a, b))
     assert sorted(heads_seen) == list(range(cfg.n_heads))   # every head exactly once
     assert sorted(items_seen) == list(range(10))            # every prompt exactly once
+
+
+# ----------------------------------------------------------- site-sharded sweeps
+class OracleEngine:
+    """Stands in for ``tvr_amd.Model`` on CPU ranks: the three engine entry
+    points the experiment layer calls (``_sweep_trace``, ``forward_clean``,
+    ``patch_sweep`` with ADD_ATTN_OUT_LASTPOS sites) computed by the oracle
+    one prompt / site at a time, so experiments.py's own site partition and
+    gather code runs unchanged under gloo."""
+
+    def __init__(self, oracle):
+        self.o, self.cfg, self.tokenizer = oracle, oracle.cfg, oracle.tokenizer
+        self.device = torch.device("cpu")
+
+    def to_single_token(self, s):
+        return self.o.to_single_token(s)
+
+    def to_string(self, t):
+        return self.o.to_string(t)
+
+    def to_tokens(self, s, prepend_bos=True):
+        return self.o.to_tokens(s, prepend_bos)
+
+    def _sweep_trace(self, n, t):
+        return {}
+
+    @staticmethod
+    def _outs(logits, targets, topk):
+        out = {}
+        if targets is not None:
+            out["prob"] = torch.stack([torch.softmax(l, 0)[t] for l, t in zip(logits, targets)]).float()
+        if topk:
+            out["topk"] = torch.stack([torch.topk(l, topk).indices for l in logits]).int()
+        return out
+
+    def forward_clean(self, seqs, targets=None, topk=0, trace=None, **kw):
+        trace["seqs"] = seqs
+        return self._outs([self.o.forward(torch.tensor([s]))[0, -1] for s in seqs], targets, topk)
+
+    def patch_sweep(self, trace, sites, vectors, topk=0, want_prob=True, **kw):
+        from oracle import reference_experiments as R
+        logits = []
+        for s in sites:
+            v = vectors[int(s["vec"])].to(self.o.dtype)
+            logits.append(self.o.run_with_hooks(torch.tensor([trace["seqs"][int(s["seq"])]]), fwd_hooks=[
+                (f"blocks.{int(s['layer'])}.hook_attn_out", lambda hv, hook, v=v: R.layer_addition_hook(hv, hook, v))])[0, -1])
+        return self._outs(logits, [int(s["target"]) for s in sites] if want_prob else None, topk)
+
+
+def _site_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tvr_amd import distributed as D
+        out = _site_sweeps(dist.group.WORLD)
+        # uneven shares (5 items, world 2/3): every rank joins the gather with its padded share
+        part = torch.tensor([[i, 10 * i] for i in D.strided_shard(5, rank, world)], dtype=torch.int32).view(-1, 2)
+        out["gather"] = D.gather_strided(part, 5)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _site_sweeps(group):
+    import tvr_amd
+    from tvr_amd import distributed as D
+    from conftest import TINY_STD, make_oracle
+    cfg = tvr_amd.get_config("tiny")
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=TINY_STD)
+    eng = OracleEngine(make_oracle(cfg, sd, tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab), torch.float64))
+    g = torch.Generator().manual_seed(3)
+    layered = torch.randn(cfg.n_layers, cfg.d_model, generator=g)
+    fv = torch.randn(cfg.d_model, generator=g) * 3
+    ctx = tvr_amd.tasks.letter_to_caps[:9]
+    kw = {} if group is None else {"group": group}
+    if group is None:
+        from tvr_amd import experiments as E
+        return {"acc": E.apply_layered_vectors_to_zero_shot(layered, ctx, "→", eng),
+                "acc_pl": E.apply_layered_vectors_to_zero_shot(layered, ctx, "→", eng, reference_late_binding=False),
+                "dp": E.apply_layered_vectors_to_zero_shot_by_probability(layered, ctx, "→", eng),
+                "fv": E.check_accuracy_of_added_task_vector_by_layer(fv, ctx, 3, eng)}
+    return {"acc": D.apply_layered_vectors_to_zero_shot_sharded(layered, ctx, "→", eng, **kw),
+            "acc_pl": D.apply_layered_vectors_to_zero_shot_sharded(layered, ctx, "→", eng, False, **kw),
+            "dp": D.apply_layered_vectors_to_zero_shot_by_probability_sharded(layered, ctx, "→", eng, **kw),
+            "fv": D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, ctx, 3, eng, **kw)}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_site_sharded_injection_sweeps_match_single_process(world):
+    """The layer sweeps (a4 accuracy, a5 Δprob) and the per-layer FV top-k
+    accuracy with (prompt, layer) sites round-robin over gloo ranks + one
+    all_gather == the same experiment code in one process == the reference
+    loop restated by the oracle."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_site_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = _site_sweeps(None)
+    import tvr_amd
+    from conftest import TINY_STD, make_oracle
+    from oracle import reference_experiments as R
+    cfg = tvr_amd.get_config("tiny")
+    oracle = make_oracle(cfg, tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=TINY_STD),
+                         tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab), torch.float64)
+    g = torch.Generator().manual_seed(3)
+    layered = torch.randn(cfg.n_layers, cfg.d_model, generator=g).double()
+    assert single["acc"] == R.apply_layered_vectors_to_zero_shot(layered, tvr_amd.tasks.letter_to_caps[:9], "→",
+                                                                 oracle)
+    for rank, out in results:
+        assert out["acc"] == single["acc"] and out["acc_pl"] == single["acc_pl"] and out["fv"] == single["fv"]
+        torch.testing.assert_close(out["dp"], single["dp"], rtol=0, atol=0)
+        assert out["gather"].tolist() == [[i, 10 * i] for i in range(5)]

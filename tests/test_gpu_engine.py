@@ -545,17 +545,21 @@ def test_batched_fv_helpers_match_reference_loops(tiny_model, tiny_oracle, mean_
     by_layer = tvr_amd.experiments.check_accuracy_of_added_task_vector_by_layer(fv, ctx, 5, model=tiny_model)
     assert by_layer == [R.check_accuracy_of_added_task_vector(fv_ref, l, ctx, 5, tiny_oracle)
                         for l in range(tiny_oracle.cfg.n_layers)]
-    if torch.equal(torch.topk(cie.cpu().flatten(), 8).indices, torch.topk(cie_ref.flatten(), 8).indices):
-        grid = tvr_amd.experiments.function_vector_head_count_grid(ours_mean * 4, cie, ctx, model=tiny_model,
-                                                                   heads_per_batch=1, number_of_batches=6)
-        L, H = tiny_oracle.cfg.n_layers, tiny_oracle.cfg.n_heads
-        want = torch.zeros(L, 6)
-        for i in range(L):
-            for j in range(6):
-                if (j + 1) < (i + 1) * H:
-                    v = R.assemble_task_vector(ref_mean * 4, cie_ref, i, j + 1)
-                    want[i, j] = R.check_accuracy_of_added_task_vector(v, i, ctx, 5, tiny_oracle)
-        assert torch.equal(grid, want)
+    # the grid from the SAME CIE on both sides (the head ranking is an input,
+    # so the comparison always runs); skipped cells keep the zero vector and
+    # are still evaluated, as scratch2.py:413-424 does
+    grid = tvr_amd.experiments.function_vector_head_count_grid(ref_mean.cuda() * 4, cie_ref.cuda(), ctx,
+                                                               model=tiny_model, heads_per_batch=1,
+                                                               number_of_batches=6)
+    L, H = tiny_oracle.cfg.n_layers, tiny_oracle.cfg.n_heads
+    want = torch.zeros(L, 6)
+    for i in range(L):
+        for j in range(6):
+            v = torch.zeros(tiny_oracle.cfg.d_model)
+            if (j + 1) < (i + 1) * H:
+                v = R.assemble_task_vector(ref_mean * 4, cie_ref, i, j + 1)
+            want[i, j] = R.check_accuracy_of_added_task_vector(v, i, ctx, 5, tiny_oracle)
+    assert torch.equal(grid, want)
 
 
 def test_x2f16_range_error_is_loud(tiny_cfg, tokenizer):
@@ -656,3 +660,28 @@ def test_profile_counts_gemm_and_hbm_kernels(tiny_model):
         assert hbm[k]["launches"] > 0 and hbm[k]["bytes"] > 0 and hbm[k]["gbps"] > 0, k
     assert hbm["capture"]["launches"] == 0
     assert hbm["entry"]["launches"] <= L  # one injection launch per entry layer
+
+
+def test_string_prompt_paths_with_bpe_tokenizer(tiny_cfg, tiny_sd):
+    """The reference's string-prompt paths (to_tokens with BOS, multi-token
+    answers, decoded-string accuracy) through a byte-level BPE tokenizer.json
+    (tests/golden/make_tokenizer.py): CIE on state -> capital prompts and the
+    FV top-5 accuracy, engine vs oracle with the same tokenizer."""
+    from pathlib import Path
+    from conftest import make_oracle
+    tok = tvr_amd.tokenizer.HFTokenizer(Path(__file__).parent / "golden" / "tokenizer.json")
+    model = tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tok)
+    oracle = make_oracle(tiny_cfg, tiny_sd, tok)
+    task = list(tvr_amd.tasks.state_to_capital_task)
+    random.seed(8)
+    mean = R.generate_mean_activation(task, ":", ",", model=oracle, num_contexts=16, len_contexts=3)
+    random.seed(9)
+    prompts, answers = tvr_amd.generate_shuffled_prompts(task, model, 3, 3, ":", ",")
+    assert all(isinstance(p, str) for p in prompts) and any(len(a) > 1 for a in answers)
+    cie = tvr_amd.calculate_average_causal_indirect_effect(mean.cuda() * 4, prompts, answers, model=model)
+    cie_ref = R.calculate_average_causal_indirect_effect(mean * 4, prompts, answers, oracle)
+    assert (cie.cpu().double() - cie_ref.double()).abs().max().item() <= 1e-4 * cie_ref.abs().max().item() + 1e-7
+    fv = R.assemble_task_vector(mean, cie_ref, 1, 3) * 4
+    ctx = task[:20]
+    assert tvr_amd.check_accuracy_of_task_vector(fv.cuda(), 1, ctx, model=model) == \
+        R.check_accuracy_of_task_vector(fv, 1, ctx, model=oracle)

@@ -15,25 +15,31 @@ T = tvr_amd.tasks
 
 
 class TokModel(tvr_amd.tokenizer.TokenizerMixin):
-    def __init__(self, vocab):
-        self.tokenizer = tvr_amd.tokenizer.SyntheticTokenizer(vocab)
+    def __init__(self, tokenizer):
+        self.tokenizer = tokenizer
         self.device = "cpu"
 
 
-M = TokModel(FIX["vocab"])
+M = TokModel(tvr_amd.tokenizer.SyntheticTokenizer(FIX["vocab"]))
+# the same reference functions on a byte-level BPE vocabulary (tests/golden/make_tokenizer.py)
+MODELS = {None: M, "hf": TokModel(tvr_amd.tokenizer.HFTokenizer(Path(__file__).parent / "golden" / "tokenizer.json"))}
 
 
 def cases(fn):
     return [c for c in FIX["cases"] if c["fn"] == fn]
 
 
+def cid(c):
+    return f"{c['fn']}-{c['seed']}-{c.get('tokenizer', 'synthetic')}"
+
+
 def as_pairs(x):
     return [tuple(p) for p in x]
 
 
-@pytest.mark.parametrize("c", cases("mix_contexts_and_query") + cases("mix_multitoken_contexts_and_query"),
-                         ids=lambda c: f"{c['fn']}-{c['seed']}")
+@pytest.mark.parametrize("c", cases("mix_contexts_and_query") + cases("mix_multitoken_contexts_and_query"), ids=cid)
 def test_icl_layouts(c):
+    M = MODELS[c.get("tokenizer")]
     demos, q, f, sep = c["args"]
     demos = as_pairs(demos)
     if c["fn"] == "mix_contexts_and_query":
@@ -44,8 +50,9 @@ def test_icl_layouts(c):
         assert R.mix_multitoken_contexts_and_query(demos, q, f, sep, M) == c["out"]
 
 
-@pytest.mark.parametrize("c", cases("generate_shuffled_prompts"), ids=lambda c: str(c["seed"]))
+@pytest.mark.parametrize("c", cases("generate_shuffled_prompts"), ids=cid)
 def test_generate_shuffled_prompts(c):
+    M = MODELS[c.get("tokenizer")]
     task, n, k, f, sep = c["args"]
     want_p, want_a = c["out"]
     random.seed(c["seed"])
@@ -56,7 +63,7 @@ def test_generate_shuffled_prompts(c):
     assert p == want_p and a == want_a
 
 
-@pytest.mark.parametrize("c", cases("assemble_end_list_tasks"), ids=lambda c: str(c["seed"]))
+@pytest.mark.parametrize("c", cases("assemble_end_list_tasks"), ids=cid)
 def test_assemble_end_list_tasks(c):
     n, k, sep = c["args"]
     want, want_mutated = c["out"]
@@ -69,8 +76,7 @@ def test_assemble_end_list_tasks(c):
 
 
 def test_construct_helpers():
-    (c1,) = cases("construct_context")
-    (c2,) = cases("construct_query")
+    c1, c2 = cases("construct_context")[0], cases("construct_query")[0]
     assert tvr_amd.prompts.construct_context(tuple(c1["args"][0]), c1["args"][1]) == c1["out"]
     assert list(tvr_amd.prompts.construct_query(tuple(c2["args"][0]), c2["args"][1])) == c2["out"]
 
