@@ -153,27 +153,39 @@ def cpu_baseline(args, cfg, prompts, answers, mean, model):
     from oracle import reference_experiments as R
     from tvr_amd.experiments import causal_indirect_effect_sums
 
-    cores = len(os.sched_getaffinity(0))
+    # every core this process may use.  On the GPU box the
+    # affinity mask shows the whole machine while the job's CPU share is
+    # OMP_NUM_THREADS (16 per GPU): more threads than that only oversubscribe.
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    cores = max(1, min(affinity, share))
     torch.set_num_threads(cores)
     t0 = time.time()
-    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0)
+    # the engine's weights: the same seeded generator on the same device (synth_engine_weights),
+    # processed there by the oracle's own TransformerLens restatement, then moved to the CPU
+    shapes = tvr_amd.weights.hf_param_shapes(cfg)
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, model.device) for n, s in shapes.items()}
     oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
                                              cfg.rotary_dim, cfg.n_ctx), sd, tokenizer=None)
     del sd
+    torch.cuda.empty_cache()
     log(f"cpu baseline: oracle weights ready in {time.time() - t0:.1f}s")
     layers = sorted({0, cfg.n_layers // 2, cfg.n_layers - 1})
     heads = list(range(cfg.n_heads))
     mean_cpu = mean.detach().cpu()
+    cie_ref = torch.zeros(cfg.n_layers, cfg.n_heads)
     t0 = time.perf_counter()
-    cie_ref = R.calculate_average_causal_indirect_effect(mean_cpu, [prompts[0]], [[answers[0]]], oracle,
-                                                         layers=layers, heads=heads)
+    for l in layers:  # the reference loop, one layer at a time for progress lines
+        cie_ref += R.calculate_average_causal_indirect_effect(mean_cpu, [prompts[0]], [[answers[0]]], oracle,
+                                                              layers=[l], heads=heads)
+        log(f"cpu baseline: layer {l} x {len(heads)} heads done at {time.perf_counter() - t0:.1f}s")
     dt = time.perf_counter() - t0
     n_sites = len(layers) * len(heads)
     out = {"value": n_sites / dt, "unit": "patched prompts/s", "cores": cores, "kind": "port",
            "sample": (f"oracle fp32 CPU (TransformerLens semantics, batch-1 hooked forward per site, reference loop "
                       f"scratch2.py:181-194): prompt 0 (T={len(prompts[0])}), layers {layers} x all {len(heads)} "
-                      f"heads = {n_sites} sites + 1 clean forward in {dt:.1f}s on {cores} threads "
-                      f"(torch.set_num_threads(len(os.sched_getaffinity(0))))")}
+                      f"heads = {n_sites} sites + {len(layers)} clean forwards in {dt:.1f}s on {cores} threads "
+                      f"(torch.set_num_threads(min(len(os.sched_getaffinity(0)) = {affinity}, OMP_NUM_THREADS = {share})))")}
     # parity on the same sites: engine vs oracle
     logits_ref = oracle.forward(torch.tensor([prompts[0]]))[0, -1]
     clean = model.forward_clean([prompts[0]], targets=[answers[0]], topk=1, return_logits=True)

@@ -73,7 +73,7 @@ def tl_process_weights(sd: Dict[str, torch.Tensor], cfg: OracleConfig, dtype=tor
         }
         blocks.append(b)
     out["W_U"] = g("embed_out.weight").T.contiguous()  # [d, V]
-    out["b_U"] = torch.zeros(cfg.d_vocab, dtype=dtype)
+    out["b_U"] = torch.zeros(cfg.d_vocab, dtype=dtype, device=out["W_U"].device)
     lnf_w, lnf_b = g("gpt_neox.final_layer_norm.weight"), g("gpt_neox.final_layer_norm.bias")
 
     # --- fold_ln (biases first, then weights, then centre read-in weights) ---
@@ -108,6 +108,14 @@ def tl_process_weights(sd: Dict[str, torch.Tensor], cfg: OracleConfig, dtype=tor
     return out
 
 
+def _cpu(x):
+    if isinstance(x, dict):
+        return {k: _cpu(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_cpu(v) for v in x]
+    return x.cpu() if isinstance(x, torch.Tensor) else x
+
+
 HookFn = Callable[[torch.Tensor, "HookPoint"], Optional[torch.Tensor]]
 
 
@@ -127,7 +135,9 @@ class HookedPythiaOracle:
                  dtype=torch.float32, tokenizer=None):
         self.cfg = cfg
         self.dtype = dtype
-        self.w = tl_process_weights(hf_state_dict, cfg, dtype)
+        # processed where the state dict lives (a GPU-resident one processes in
+        # seconds), then kept on the CPU: the oracle always runs on the CPU
+        self.w = _cpu(tl_process_weights(hf_state_dict, cfg, dtype))
         self.tokenizer = tokenizer
         self._hooks: Dict[str, List[HookFn]] = {}
         self._cache: Optional[ActivationCache] = None

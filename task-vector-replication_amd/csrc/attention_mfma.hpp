@@ -17,9 +17,11 @@
 // rotary_pct 0.25; the host checks it) stay inside lane group 0, at
 // compile-time register indices.  f32-input MFMA is exact fp32
 // (a k-ordered fmaf chain per step); the dot products are summed in a permuted
-// k order relative to a sequential loop, i.e. within fp32 rounding of
-// attention_kernel (kernels.hpp), whose TransformerLens semantics this keeps:
+// k order relative to a sequential loop, i.e. within fp32 rounding of the
+// TransformerLens attention (oracle/hooked_pythia.py _attn):
 // scores q.k / sqrt(d_head), -inf causal mask, fp32 softmax, z = P V.
+// (It replaced an LDS-staged block-per-(sequence, head) kernel, 1.21 -> 0.45
+// ms per launch at C3: DESIGN.md section 3.3.)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>

@@ -109,7 +109,6 @@ struct tvr_model {
   int gemm_mode = TVR_GEMM_F32;
   uint16_t* planes = nullptr;
   unsigned* range_flag = nullptr;  // device word: X2F16 input out of range since the last status read
-  bool att_mfma = true;            // attention_mfma_kernel where it applies (env TVR_ATTENTION=lds: the LDS kernel)
   std::vector<MatW> w1, w2;
   MatW wu;
   char* ws = nullptr;
@@ -259,34 +258,12 @@ struct ProfSpan {
   }
 };
 
-// Planar launches run gemm_pingpong_kernel (split-K below 192 tiles; measured
-// faster than the 128x128 tile at every size the sweeps produce);
-// TVR_GEMM_SCHED=planar selects gemm_planar_kernel (256x256 from 512 tiles,
-// else 128x128) instead, for A/B runs.
-bool gemm_pingpong_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("TVR_GEMM_SCHED");
-    return !(e && std::string(e) == "planar");
-  }();
-  return on;
-}
-// A/B knobs of the planar launch policy (default both on): TVR_GEMM_SPLITK=0
-// disables split-K, TVR_GEMM_PP_SMALL=0 sends launches below 512 tiles to the
-// 128x128 gemm_planar_kernel instead of gemm_pingpong_kernel.
+// TVR_PREFIX_SHARE=0 turns off shared-prefix rows in tvr_forward_clean /
+// tvr_patch_sweep (read per call; the tests run both settings and compare).
 bool env_flag(const char* name) {
   const char* e = getenv(name);
   return !(e && std::string(e) == "0");
 }
-bool gemm_splitk_enabled() {
-  static const bool on = env_flag("TVR_GEMM_SPLITK");
-  return on;
-}
-bool gemm_pp_small_enabled() {
-  static const bool on = env_flag("TVR_GEMM_PP_SMALL");
-  return on;
-}
-// TVR_PREFIX_SHARE=0 turns off shared-prefix rows in tvr_patch_sweep (A/B and
-// tests; read per call).
 bool prefix_share_enabled() { return env_flag("TVR_PREFIX_SHARE"); }
 
 // Activation format of the model's GEMM inputs (split.hpp).
@@ -300,33 +277,32 @@ int act_fmt(const tvr_model* m) {
 // there are at most 16 block columns (tools/gemm_split_probe x2ppgm<N>: at
 // M = 90,000 the qkv shape ran 459 / 451 / 419 TF at 4 / 8 / 16, the
 // MLP-out shape (10 columns) 470 / 466 / 458 at 2 / 4 / 8).
-int pp_group_m(int N) {
-  static const int forced = [] {  // TVR_GEMM_GROUP=<g> forces one group size (A/B)
-    const char* e = getenv("TVR_GEMM_GROUP");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  if (forced > 0) return forced;
-  return (N + 255) / 256 <= 16 ? 2 : 4;
-}
+int pp_group_m(int N) { return (N + 255) / 256 <= 16 ? 2 : 4; }
 
 void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
-               const GemmEpi& ep0, float acc_scale, int tile_base, int count, hipStream_t st) {
+               const GemmEpi& ep0, float acc_scale, int tile_base, int count, bool vec, hipStream_t st) {
   GemmEpi ep = ep0;
   ep.tile_base = tile_base;
   ep.tile_count = count;
   ep.group_m = pp_group_m(N);
   const dim3 g(count > 0 ? count : gemm_pingpong_grid(M, N));
-#define TVR_PP1(E, F) \
-  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
+#define TVR_PP1(E, F, V) \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
                      ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_PP1V(E, F) \
+  if (vec) { TVR_PP1(E, F, true); } else { TVR_PP1(E, F, false); }
 #define TVR_PP1F(E) \
-  if (a_fmt == ACT_X2F16) { TVR_PP1(E, ACT_X2F16); } else { TVR_PP1(E, ACT_BF16); }
+  if (a_fmt == ACT_X2F16) { TVR_PP1V(E, ACT_X2F16); } else { TVR_PP1V(E, ACT_BF16); }
   switch (epi) {
     case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
     case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
+    case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked)
+      if (a_fmt == ACT_X2F16) { TVR_PP1(EPI_STATS, ACT_X2F16, true); } else { TVR_PP1(EPI_STATS, ACT_BF16, true); }
+      break;
     default: TVR_PP1F(EPI_RESID); break;
   }
 #undef TVR_PP1F
+#undef TVR_PP1V
 #undef TVR_PP1
 }
 
@@ -379,10 +355,6 @@ struct PpPlan {
   int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
   int tail_split = 1;
 };
-bool gemm_tail_enabled() {
-  static const bool on = env_flag("TVR_GEMM_TAIL");
-  return on;
-}
 PpPlan plan_pp(int M, int N, int K, int a_fmt) {
   PpPlan p;
   const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_BF16 ? 64 : 32);
@@ -392,7 +364,7 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt) {
   }
   const int rounds = (tiles + 255) / 256;
   const int tb = tiles - 256 * (rounds - 1);
-  if (rounds < 2 || tb > 224 || !gemm_tail_enabled()) return p;
+  if (rounds < 2 || tb > 224) return p;
   int best = 1;
   double br = 1.0;
   for (int s = 2; s <= 16 && nkt / s >= 8; ++s) {
@@ -413,9 +385,13 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt) {
   return p;
 }
 
-// C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] (a_fmt ACT_F32) or a
-// planar activation format (split.hpp: lda logical elements per row), which
-// needs the same format's weight planes (W.h) and runs gemm_planar_kernel.
+// C = A @ W^T with epilogue `epi`.  A is fp32 [M][lda] (a_fmt ACT_F32:
+// gemm_f32_nt_kernel, or the in-GEMM splits of the primitive ABI entry points
+// when W carries x3bf16 / x2f16 planes) or a planar activation format
+// (split.hpp: lda logical elements per row) with the same format's weight
+// planes (W.h): gemm_pingpong_kernel, split-K below 192 tiles and a split last
+// round when it pays (plan_pp; not for EPI_STATS, whose statistics exist only
+// in the whole-K LDS epilogue).
 int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int ldw, int M, int N,
                 int K, const GemmEpi& ep, hipStream_t st, tvr_model* m = nullptr,
                 unsigned* range_flag = nullptr) {
@@ -426,6 +402,9 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     return fail(TVR_ERR_INVALID, "gemm: the activation-format GELU epilogue belongs to the planar paths");
   if (epi == EPI_SPLIT_GELU && planar)
     return fail(TVR_ERR_INVALID, "gemm: planar paths write GELU columns in their activation format");
+  if (epi == EPI_STATS && (!planar || N % 4 != 0 || !ep.stats))
+    return fail(TVR_ERR_INVALID, "gemm: the fused statistics epilogue needs a planar format, N % 4 == 0 and a "
+                                 "statistics buffer");
   if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0) ||
       (a_fmt == ACT_BF16 && K % 64 != 0))
     return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes, K of 64 for "
@@ -436,92 +415,66 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     ev1 = prof_event(m);
     if (ev0) TVR_HIP(hipEventRecord(ev0, st));
   }
-  const bool large = gemm_use_large(M, N);
+  const float acc_scale = (a_fmt == ACT_BF16) ? 1.0f : 1.0f / (W.wscale * X2_ASCALE);
+  if (planar) {
+    const uint16_t* Ah = static_cast<const uint16_t*>(A);
+    const bool vec = planar_epilogue_vec(epi, ep, N);
+    PpPlan plan;
+    if (m && vec && epi != EPI_STATS) plan = plan_pp(M, N, K, a_fmt);
+    if (plan.ksplit > 1) {
+      TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, gemm_pingpong_grid(M, N),
+                               plan.ksplit, m, st));
+    } else if (plan.tail_base > 0) {
+      launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, true, st);
+      TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
+                               gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st));
+    } else {
+      launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, 0, vec, st);
+    }
+  } else {
+    const float* Af = static_cast<const float*>(A);
+    unsigned* flag = m ? m->range_flag : range_flag;
+    const bool large = gemm_use_large(M, N);
 #define TVR_GEMM_LAUNCH(E, TL)                                                                  \
   hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Af, lda, W.f, ldw, M, N, K, ep)
 #define TVR_X3_LAUNCH(E, TL)                                                                      \
   hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
                      0, st, Af, lda, W.x, ldw, W.wps, M, N, K, ep)
-  unsigned* flag = m ? m->range_flag : range_flag;
-  const float acc_scale = (a_fmt == ACT_BF16) ? 1.0f : 1.0f / (W.wscale * X2_ASCALE);
-  const float* Af = static_cast<const float*>(A);
-  const uint16_t* Ah = static_cast<const uint16_t*>(A);
-  const bool vec = planar_epilogue_vec(epi, ep, N);
-  const bool pingpong = gemm_pingpong_enabled(), pp_small = gemm_pp_small_enabled();
-#define TVR_PL_LAUNCH2(E, TL, F, V)                                                                         \
-  hipLaunchKernelGGL((gemm_planar_kernel<E, TL, F, V>), dim3(gemm_planar_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
-                     st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
-#define TVR_PL_LAUNCH1(E, TL, F) \
-  if (vec) TVR_PL_LAUNCH2(E, TL, F, true); else TVR_PL_LAUNCH2(E, TL, F, false)
-  GemmEpi epp = ep;  // whole-launch pingpong: the same raster group as launch_pp
-  epp.group_m = pp_group_m(N);
-#define TVR_PP_LAUNCH2(E, F, V)                                                                              \
-  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), dim3(gemm_pingpong_grid(M, N)), dim3(PP_THREADS), 0, st, \
-                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, epp)
-#define TVR_PL_LARGE(E, F)                                                   \
-  if (pingpong) {                                                            \
-    if (vec) TVR_PP_LAUNCH2(E, F, true); else TVR_PP_LAUNCH2(E, F, false);  \
-  } else {                                                                   \
-    TVR_PL_LAUNCH1(E, PlanarLarge, F);                                       \
-  }
-#define TVR_PL_LAUNCH(E)                                                                               \
-  if (a_fmt == ACT_X2F16) {                                                                              \
-    if (large || (pingpong && pp_small)) { TVR_PL_LARGE(E, ACT_X2F16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_X2F16); } \
-  } else {                                                                                               \
-    if (large || (pingpong && pp_small)) { TVR_PL_LARGE(E, ACT_BF16); } else { TVR_PL_LAUNCH1(E, PlanarSmall, ACT_BF16); }   \
-  }
 #define TVR_X2_LAUNCH(E, TL)                                                                         \
   hipLaunchKernelGGL((gemm_x2f16_nt_kernel<E, TL>), dim3(gemm_x2_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
                      st, Af, lda, W.h, ldw, W.wps, acc_scale, flag, M, N, K, ep)
-#define TVR_GEMM_PICK_NP(E)                                 \
-  if (W.h) {                                                \
+#define TVR_GEMM_PICK(E)                                                          \
+  if (W.h) {                                                                      \
     if (large) TVR_X2_LAUNCH(E, X2Large); else TVR_X2_LAUNCH(E, X2Small);         \
-  } else if (W.x) {                                         \
+  } else if (W.x) {                                                               \
     if (large) TVR_X3_LAUNCH(E, X3Large); else TVR_X3_LAUNCH(E, X3Small);         \
-  } else {                                                  \
+  } else {                                                                        \
     if (large) TVR_GEMM_LAUNCH(E, TileLarge); else TVR_GEMM_LAUNCH(E, TileSmall); \
   }
-#define TVR_GEMM_PICK(E) \
-  if (planar) { TVR_PL_LAUNCH(E); } else { TVR_GEMM_PICK_NP(E); }
-  // planar launches on the pingpong kernel with a model: split-K / tail split (plan_pp)
-  PpPlan plan;
-  if (planar && pingpong && m && vec && gemm_splitk_enabled()) plan = plan_pp(M, N, K, a_fmt);
-  if (plan.ksplit > 1) {
-    const int rc = launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0,
-                                    gemm_pingpong_grid(M, N), plan.ksplit, m, st);
-    if (rc != TVR_OK) return rc;
-  } else if (plan.tail_base > 0) {
-    launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, st);
-    const int rc = launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
-                                    gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st);
-    if (rc != TVR_OK) return rc;
-  } else
-  switch (epi) {
-    case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
-    case EPI_SPLIT_GELU: TVR_GEMM_PICK_NP(EPI_SPLIT_GELU); break;
-    case EPI_SPLIT_GELU_ACT: TVR_PL_LAUNCH(EPI_SPLIT_GELU_ACT); break;
-    default: TVR_GEMM_PICK(EPI_RESID); break;
-  }
+    switch (epi) {
+      case EPI_BIAS: TVR_GEMM_PICK(EPI_BIAS); break;
+      case EPI_SPLIT_GELU: TVR_GEMM_PICK(EPI_SPLIT_GELU); break;
+      default: TVR_GEMM_PICK(EPI_RESID); break;
+    }
 #undef TVR_GEMM_PICK
-#undef TVR_GEMM_PICK_NP
-#undef TVR_X3_LAUNCH
 #undef TVR_X2_LAUNCH
-#undef TVR_PL_LAUNCH
-#undef TVR_PL_LARGE
-#undef TVR_PP_LAUNCH2
-#undef TVR_PL_LAUNCH1
-#undef TVR_PL_LAUNCH2
+#undef TVR_X3_LAUNCH
 #undef TVR_GEMM_LAUNCH
+  }
   TVR_HIP(hipGetLastError());
   if (ev0 && ev1) {
     TVR_HIP(hipEventRecord(ev1, st));
     // minimal operand bytes: W read once (fp32 4, 3 bf16 planes 6, 2 fp16 planes 4, bf16 2 B per element),
     // A once in its format (fp32 / x2f16 4, bf16 2), C once as fp32
+    // (EPI_STATS: the per-tile statistics records instead of C)
     const double wbytes = W.x ? 6.0 : (a_fmt == ACT_BF16 ? 2.0 : 4.0);
     const double abytes = a_fmt == ACT_BF16 ? 2.0 : 4.0;
-    m->prof_recs.push_back({ev0, ev1, epi == EPI_SPLIT_GELU_ACT ? (int)EPI_SPLIT_GELU : epi, 2.0 * M * N * (double)K,
-                            abytes * M * (double)K + 4.0 * M * (double)N + wbytes * N * (double)K});
+    const double cbytes = epi == EPI_STATS ? 4.0 * M * (double)ep.stats_tiles * (2 + 2 * ep.stats_k)
+                                           : 4.0 * M * (double)N;
+    const int kind = epi == EPI_SPLIT_GELU_ACT ? (int)EPI_SPLIT_GELU : epi == EPI_STATS ? (int)EPI_BIAS : epi;
+    m->prof_recs.push_back({ev0, ev1, kind, 2.0 * M * N * (double)K,
+                            abytes * M * (double)K + cbytes + wbytes * N * (double)K});
   }
   return TVR_OK;
 }
@@ -558,9 +511,9 @@ struct Acts {
 };
 
 // z: the z columns of a2 (fp32 or activation format fmt); zf: optional fp32 copy [rows][d].
-// attention_mfma_kernel (one wave per (sequence, head), fp32 MFMA, no LDS)
-// for the Pythia head sizes (d_head 16 (tiny), 64, 80, 128) with
-// rotary_dim = d_head / 4 (every Pythia: rotary_pct 0.25), else attention_kernel.
+// attention_mfma_kernel (one wave per (sequence, head), fp32 MFMA, no LDS) for
+// the Pythia head sizes d_head 16 (tiny), 64, 80, 128 with rotary_dim =
+// d_head / 4 (every Pythia: rotary_pct 0.25); check_config rejects the rest.
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
                      int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st) {
   if (n_seqs <= 0) return TVR_OK;
@@ -568,10 +521,9 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const int d = c.d_model;
   const float inv_scale = 1.0f / std::sqrt((float)c.d_head);
   const int dh = c.d_head;
-  if (m->att_mfma && c.rotary_dim == dh / 4 && (dh == 16 || dh == 64 || dh == 80 || dh == 128)) {
-    const int pairs = n_seqs * c.n_heads;
-    const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
-    const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : 8;
+  const int pairs = n_seqs * c.n_heads;
+  const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
+  const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : 8;
 #define TVR_ATTM(F, DHV, NK)                                                                                        \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d, inv_scale)
@@ -583,36 +535,16 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
 #define TVR_ATTM_DH(F)                                                                          \
   if (dh == 16) { TVR_ATTM_NK(F, 16); } else if (dh == 64) { TVR_ATTM_NK(F, 64); }              \
   else if (dh == 80) { TVR_ATTM_NK(F, 80); } else { TVR_ATTM_NK(F, 128); }
-    if (fmt == ACT_X2F16) {
-      TVR_ATTM_DH(ACT_X2F16);
-    } else if (fmt == ACT_BF16) {
-      TVR_ATTM_DH(ACT_BF16);
-    } else {
-      TVR_ATTM_DH(ACT_F32);
-    }
+  if (fmt == ACT_X2F16) {
+    TVR_ATTM_DH(ACT_X2F16);
+  } else if (fmt == ACT_BF16) {
+    TVR_ATTM_DH(ACT_BF16);
+  } else {
+    TVR_ATTM_DH(ACT_F32);
+  }
 #undef TVR_ATTM_DH
 #undef TVR_ATTM_NK
 #undef TVR_ATTM
-    TVR_HIP(hipGetLastError());
-    return TVR_OK;
-  }
-  const size_t smem = attention_smem_bytes(maxT, c.d_head);
-#define TVR_ATT_LAUNCH(F)                                                                                     \
-  do {                                                                                                        \
-    if (smem > 64 * 1024)                                                                                     \
-      TVR_HIP(hipFuncSetAttribute((const void*)attention_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                  (int)smem));                                                                \
-    hipLaunchKernelGGL(attention_kernel<F>, dim3(n_seqs, c.n_heads), dim3(ATT_THREADS), smem, st, qkv, 3 * d,    \
-                       cache_qkv, 3 * d, d_seqs, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d,     \
-                       c.d_head, c.rotary_dim, inv_scale);                                                    \
-  } while (0)
-  if (fmt == ACT_X2F16)
-    TVR_ATT_LAUNCH(ACT_X2F16);
-  else if (fmt == ACT_BF16)
-    TVR_ATT_LAUNCH(ACT_BF16);
-  else
-    TVR_ATT_LAUNCH(ACT_F32);
-#undef TVR_ATT_LAUNCH
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }
@@ -719,15 +651,51 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
 }
 
 // Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
+// Planar modes without requested logits: the unembed GEMM's fused statistics
+// epilogue (EPI_STATS: per-tile max / sum exp / top-k candidates / target
+// logit, no [rows][V] logits in HBM) + stats_merge_kernel.  Otherwise the
+// logits are written (to out_logits, or the scratch) and row_stats_kernel
+// reads them back.
+bool final_fused(const tvr_model* m, int fmt, const float* out_logits) {
+  return fmt != ACT_F32 && !out_logits && m->cfg.d_vocab % 4 == 0;
+}
+// floats of run_final's scratch for chunks of fc rows
+size_t final_scratch_floats(const tvr_model* m, int fmt, int fc, int topk, const float* out_logits) {
+  const int V = m->cfg.d_vocab;
+  if (final_fused(m, fmt, out_logits)) return (size_t)fc * ((V + 255) / 256) * (2 + 2 * topk) + fc;
+  return out_logits ? 0 : (size_t)fc * V;
+}
+
 int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int32_t* d_targets,
-              int n, float* xf, float* logits_ws, float* out_prob, int32_t* out_topk, int topk,
+              int n, float* xf, float* scratch, float* out_prob, int32_t* out_topk, int topk,
               float* out_logits, int fmt, hipStream_t st) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model, V = c.d_vocab;
+  const bool fused = final_fused(m, fmt, out_logits);
+  const int tiles = (V + 255) / 256;
   for (int s = 0; s < n; s += kFinalChunk) {
     const int cn = std::min(kFinalChunk, n - s);
     TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m));
-    float* lg = out_logits ? out_logits + (size_t)s * V : logits_ws;
+    if (fused) {
+      float* part = scratch;
+      float* tlogit = scratch + (size_t)cn * tiles * (2 + 2 * topk);
+      GemmEpi e{};
+      e.bias = m->b_unembed;
+      e.stats = part;
+      e.stats_k = topk;
+      e.stats_tiles = tiles;
+      e.targets = d_targets ? d_targets + s : nullptr;
+      e.tlogit = tlogit;
+      TVR_TRY(launch_gemm(EPI_STATS, xf, d, fmt, m->wu, d, cn, V, d, e, st, m));
+      ProfSpan ps(m, st);
+      hipLaunchKernelGGL(stats_merge_kernel, dim3((cn + MERGE_WAVES - 1) / MERGE_WAVES), dim3(64 * MERGE_WAVES), 0,
+                         st, part, tiles, topk, tlogit, d_targets ? d_targets + s : nullptr, cn, V,
+                         out_prob ? out_prob + s : nullptr, out_topk ? out_topk + (size_t)s * topk : nullptr, topk);
+      TVR_HIP(hipGetLastError());
+      ps.done(TVR_HBM_ROW_STATS, (double)cn * (tiles * (2.0 + 2.0 * topk) + 1.0) * 4.0);  // the records + target logit
+      continue;
+    }
+    float* lg = out_logits ? out_logits + (size_t)s * V : scratch;
     GemmEpi e{};
     e.bias = m->b_unembed;
     e.out0 = lg;
@@ -753,8 +721,9 @@ int check_config(const tvr_config& c) {
     return fail(TVR_ERR_INVALID, "config: rotary_dim must be even and <= d_head");
   if (c.d_model % GEMM_BK != 0 || (c.d_model + c.d_mlp) % GEMM_BK != 0)
     return fail(TVR_ERR_UNSUPPORTED, "config: d_model and d_model + d_mlp must be multiples of 32");
-  if (c.d_head > 128 || c.d_head % 16 != 0)
-    return fail(TVR_ERR_UNSUPPORTED, "config: d_head must be a multiple of 16 and <= 128");
+  if (!(c.d_head == 16 || c.d_head == 64 || c.d_head == 80 || c.d_head == 128) || c.rotary_dim * 4 != c.d_head)
+    return fail(TVR_ERR_UNSUPPORTED, "config: the attention kernel covers the Pythia heads: d_head 16 / 64 / 80 / "
+                                     "128 with rotary_dim = d_head / 4");
   return TVR_OK;
 }
 
@@ -785,7 +754,6 @@ int tvr_model_create(const tvr_config* cfg, const float* w_embed, const tvr_laye
   m->layers.assign(layers, layers + cfg->n_layers);
   m->w_unembed_t = w_unembed_t;
   m->b_unembed = b_unembed;
-  if (const char* a = std::getenv("TVR_ATTENTION")) m->att_mfma = std::string(a) != "lds";
   for (int l = 0; l < cfg->n_layers; ++l) {
     m->w1.push_back(MatW{layers[l].w1});
     m->w2.push_back(MatW{layers[l].w2});
@@ -1065,8 +1033,6 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
       return fail(TVR_ERR_INVALID, "token id " + std::to_string(tokens[r]) + " out of range");
   if (trace && (n_seq > trace->max_seqs || R > trace->max_tokens))
     return fail(TVR_ERR_INVALID, "trace capacity exceeded");
-  if (attention_smem_bytes(maxT, c.d_head) > 160 * 1024)
-    return fail(TVR_ERR_UNSUPPORTED, "attention LDS budget exceeded");
 
   std::vector<SeqDesc> seqs(n_seq);
   for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1, 0, 0};
@@ -1122,7 +1088,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   const size_t o_qkv = trace ? 0 : cv.take<float>((size_t)R * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
-  const size_t o_lg = out_logits ? 0 : cv.take<float>((size_t)FC * c.d_vocab);
+  const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, topk, out_logits));
   const size_t o_cap = capture_zsum ? cv.take<float>((size_t)CAP_GROUPS * d) : 0;
   // fp32 hook_z for the capture when no trace slot receives it
   const size_t o_zf = (capture_zsum && !trace) ? cv.take<float>((size_t)R * d) : 0;
@@ -1187,8 +1153,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   }
   if (out_prob || out_topk || out_logits)
     TVR_TRY(run_final(m, a.resid, d_last, (const int32_t*)(base + o_tg), n_seq, (float*)(base + o_xf),
-                      out_logits ? nullptr : (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt,
-                      st));
+                      (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st));
   return TVR_OK;
 }
 
@@ -1357,9 +1322,7 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   const size_t o_qkv = cv.take<float>((size_t)R * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
-  const size_t o_lg = out_logits ? 0 : cv.take<float>((size_t)FC * c.d_vocab);
-  if (attention_smem_bytes(maxT, c.d_head) > 160 * 1024)
-    return fail(TVR_ERR_UNSUPPORTED, "attention LDS budget exceeded");
+  const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, topk, out_logits));
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -1412,8 +1375,7 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   }
   TVR_TRY(enter(L));
   return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
-                   (float*)(base + o_xf), out_logits ? nullptr : (float*)(base + o_lg), out_prob,
-                   out_topk, topk, out_logits, fmt, st);
+                   (float*)(base + o_xf), (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st);
 }
 
 int tvr_project_heads(tvr_model* m, const float* zsum, float* out, void* stream) {

@@ -47,6 +47,11 @@ enum GemmEpiKind {
   EPI_SPLIT_GELU = 1,  // col < n_split: out0 = acc + bias ; else out1 = gelu(acc + bias)
   EPI_RESID = 2,       // out0 = acc + bias + resid   (in place allowed: out0 == resid)
   EPI_SPLIT_GELU_ACT = 3,  // EPI_SPLIT_GELU with the GELU columns in the planar activation format (split.hpp)
+  // Fused unembed statistics (gemm_pingpong_kernel only): no logits written.
+  // Per (row, 256-column tile) of acc + bias: the max, sum(exp(x - max)) and
+  // the top stats_k (value, column) candidates to stats, and the target
+  // column's logit to tlogit; stats_merge_kernel combines the tiles.
+  EPI_STATS = 4,
 };
 
 struct GemmEpi {
@@ -80,6 +85,14 @@ struct GemmEpi {
   int tile_base;
   int tile_count;
   int group_m;  // gemm_pingpong_kernel raster: m-blocks per group (0: GEMM_GROUP_M)
+  // EPI_STATS: record of (row m, column tile t) at stats + (m * stats_tiles + t) * (2 + 2 stats_k):
+  // {max, sum exp, value[stats_k], column[stats_k] (int bits)}; targets[m] (may be null) selects
+  // the logit written to tlogit[m].
+  float* stats;
+  int stats_k;
+  int stats_tiles;
+  const int32_t* targets;
+  float* tlogit;
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":

@@ -77,6 +77,53 @@ constexpr int PP_EPI_LDR = 260;                   // floats per LDS row
 constexpr bool PP_NT_STORES = TVR_PP_NT;
 constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
 
+// EPI_STATS: the rows of one LDS half (acc * acc_scale, row stride
+// PP_EPI_LDR) reduced to the per-tile statistics of GemmEpi::stats instead of
+// being stored.  Wave w takes rows w, w + 8, ...; lane l holds columns
+// 4l .. 4l+3 of the tile (+ bias b4), so every reduction is one butterfly over
+// the wave: the max, sum(exp(x - max)), and stats_k rounds of (value desc,
+// column asc) argmax with the winner removed from its lane.  The tile's
+// columns are [col0, col0 + Nlim), Nlim % 4 == 0 (host-checked).
+__device__ __forceinline__ void pp_stats_rows(const GemmEpi& ep, const float* L, int grow0, int col0, int rows,
+                                              int Nlim, f32x4 b4, int t) {
+  const int wave = t >> 6, lane = t & 63, c4 = 4 * lane;
+  const bool live = c4 < Nlim;
+  const int K = ep.stats_k, rec = 2 + 2 * K, tile = col0 >> 8;
+  for (int r = wave; r < rows; r += PP_THREADS / 64) {
+    f32x4 v = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (live) v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
+    const int m = grow0 + r;
+    const float mx = wave_max(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    float se = 0.f;
+    if (live) se = (expf(v[0] - mx) + expf(v[1] - mx)) + (expf(v[2] - mx) + expf(v[3] - mx));
+    se = wave_sum(se);
+    float* o = ep.stats + ((size_t)m * ep.stats_tiles + tile) * rec;
+    if (ep.targets && ep.tlogit && live) {
+      const int q = ep.targets[m] - col0 - c4;
+      if (q >= 0 && q < 4) ep.tlogit[m] = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+    }
+    unsigned taken = live ? 0u : 0xFu;
+    for (int j = 0; j < K; ++j) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (!((taken >> q) & 1u)) argmax_merge(bv, bi, v[q], col0 + c4 + q);
+      wave_argmax(bv, bi);
+      const int own = bi - col0 - c4;
+      if (own >= 0 && own < 4) taken |= 1u << own;
+      if (lane == 0) {
+        o[2 + j] = bv;
+        o[2 + K + j] = __int_as_float(bi);
+      }
+    }
+    if (lane == 0) {
+      o[0] = mx;
+      o[1] = se;
+    }
+  }
+}
+
 template <int EPI, int FMT, bool NOSTORE = false>
 __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (&acc)[8][4], float* L, int row0,
                                                 int col0, int Mlim, int Nlim, int wr, int wc, int lane, int t,
@@ -108,7 +155,9 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
     }
     __syncthreads();
     const int rows = min(128, Mlim - p * 128);
-    if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
+    if constexpr (EPI == EPI_STATS) {
+      pp_stats_rows(ep, L, row0 + p * 128, col0, rows, Nlim, b4, t);
+    } else if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
 #pragma unroll 2
       for (int r = t >> 5; r < 128; r += PP_THREADS / 32) {
         if (r >= rows) break;
@@ -370,29 +419,33 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     }
     return;
   }
-  if (acc_scale != 1.0f) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
-  }
-  if (S > 1) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
-    GemmEpi pe = ep;
-    pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
-    pe.ld0 = 256;
-    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M - m0, N - n0, wr * 128, wc * 64, lane);
+  if constexpr (EPI == EPI_STATS) {  // the statistics exist in the LDS epilogue only (host-checked)
+    return;
   } else {
-    gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
-  }
-  if (VAR == 6 && ep.stamps && t == 0) {
-    unsigned long long* o = ep.stamps + 4 * blockIdx.x;
-    o[0] = st0;
-    o[1] = d_loop0;
-    o[2] = d_loop1;
-    o[3] = __builtin_amdgcn_s_memtime();
-  } else if (ep.stamps && t == 0) {
-    ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
-    ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+    if (acc_scale != 1.0f) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
+    }
+    if (S > 1) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
+      GemmEpi pe = ep;
+      pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
+      pe.ld0 = 256;
+      gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M - m0, N - n0, wr * 128, wc * 64, lane);
+    } else {
+      gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(ep, acc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
+    }
+    if (VAR == 6 && ep.stamps && t == 0) {
+      unsigned long long* o = ep.stamps + 4 * blockIdx.x;
+      o[0] = st0;
+      o[1] = d_loop0;
+      o[2] = d_loop1;
+      o[3] = __builtin_amdgcn_s_memtime();
+    } else if (ep.stamps && t == 0) {
+      ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
+      ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+    }
   }
 }
 

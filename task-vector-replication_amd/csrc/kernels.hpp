@@ -45,16 +45,7 @@ struct EntryDesc {
 };
 
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+// wave_sum / wave_max: split.hpp
 
 // ---------------------------------------------------------------------------
 // hook_embed: resid[r] = W_E[tokens[r]]   (one float4 per thread)
@@ -148,128 +139,9 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
 }
 
 // ---------------------------------------------------------------------------
-// Causal attention for ragged sequences with an optional clean K/V prefix.
-// grid = (n_seqs, n_heads), block = 256 (4 waves).  The block stages K and V
-// of every position (float4 loads; prefix from the clean trace's K/V, the rest
-// from this run), rotates K in LDS, then each wave owns query rows
-// q0+wave, q0+wave+4, ... with wave-private Q/P buffers: after the one staging
-// barrier no block-level barrier remains.  One score per lane per 64 keys,
-// wave-shuffle softmax, one output dim per lane.
-//   qkv  [rows][3d]: q at h*dh, k at d + h*dh, v at 2d + h*dh (pre-rotary)
-//   z    [rows][ldz]: written at h*dh  (attn.hook_z), the next GEMM's input:
-//        fp32, or a planar activation format FMT (split.hpp; X2F16 is
-//        range-checked into flag)
-//   zf   [rows][ldzf] fp32 copy (trace / capture) or nullptr
-constexpr int ATT_THREADS = 256;
+// Longest sequence the attention kernel takes (attention_mfma.hpp: up to 8
+// key tiles of 16 in registers).
 constexpr int ATT_MAX_T = 128;
-
-// LDS ops of one wave retire in order; this only stops the compiler from
-// moving them across the point.
-__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-inline size_t attention_smem_bytes(int T, int dh) {
-  return sizeof(float) * ((size_t)2 * T * (dh + 1) + 4 * dh + 4 * T);
-}
-
-template <int FMT>
-__global__ void __launch_bounds__(ATT_THREADS)
-attention_kernel(const float* __restrict__ qkv, int ldq,
-                 const float* __restrict__ cache, int ldc,
-                 const SeqDesc* __restrict__ seqs, void* __restrict__ z, int ldz,
-                 float* __restrict__ zf, int ldzf, unsigned* __restrict__ flag,
-                 const float* __restrict__ cos_t, const float* __restrict__ sin_t,
-                 int d, int dh, int rd, float inv_attn_scale) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const SeqDesc sd = seqs[blockIdx.x];
-  const int h = blockIdx.y;
-  const int T = sd.p0 + sd.n;
-  const int dhp = dh + 1;
-  float* Ks = smem;                    // [T][dh+1]
-  float* Vs = Ks + T * dhp;            // [T][dh+1]
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  float* Qs = Vs + T * dhp + wave * dh;          // wave-private [dh]
-  float* Ps = Vs + T * dhp + 4 * dh + wave * T;  // wave-private [T]
-
-  // stage K, V (dh % 16 == 0: whole float4 per lane)
-  const int d4 = dh >> 2;
-  for (int e = t; e < T * d4; e += ATT_THREADS) {
-    const int j = e / d4, k = (e - j * d4) * 4;
-    const float* src = (j < sd.p0) ? (sd.prefix_live ? qkv + (size_t)(sd.cache_row + j) * ldq
-                                                     : cache + (size_t)(sd.cache_row + j) * ldc)
-                                   : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
-    const float4 kv = *(const float4*)(src + d + h * dh + k);
-    const float4 vv = *(const float4*)(src + 2 * d + h * dh + k);
-    float* kr = Ks + j * dhp + k;
-    float* vr = Vs + j * dhp + k;
-    kr[0] = kv.x; kr[1] = kv.y; kr[2] = kv.z; kr[3] = kv.w;
-    vr[0] = vv.x; vr[1] = vv.y; vr[2] = vv.z; vr[3] = vv.w;
-  }
-  __syncthreads();
-  // TL apply_rotary (rotate-half / non-adjacent pairs) on K, position j:
-  //   out[i] = x[i]*cos[i] - x[i+rd/2]*sin[i],  out[i+rd/2] = x[i+rd/2]*cos + x[i]*sin
-  const int half = rd >> 1;
-  for (int e = t; e < T * half; e += ATT_THREADS) {
-    const int j = e / half, i = e - j * half;
-    float* kr = Ks + j * dhp;
-    const float x0 = kr[i], x1 = kr[i + half];
-    kr[i] = x0 * cos_t[j * rd + i] - x1 * sin_t[j * rd + i];
-    kr[i + half] = x1 * cos_t[j * rd + i + half] + x0 * sin_t[j * rd + i + half];
-  }
-  __syncthreads();
-
-  for (int i = sd.q0 + wave; i < sd.n; i += 4) {
-    const int pos = sd.p0 + i;
-    const float* qsrc = qkv + (size_t)(sd.row0 + i) * ldq + h * dh;
-    for (int k = lane; k < dh; k += 64) {
-      float v = qsrc[k];
-      if (k < half) v = v * cos_t[pos * rd + k] - qsrc[k + half] * sin_t[pos * rd + k];
-      else if (k < rd) v = v * cos_t[pos * rd + k] + qsrc[k - half] * sin_t[pos * rd + k];
-      Qs[k] = v;
-    }
-    wave_lds_fence();
-    float sc[ATT_MAX_T / 64];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-      const int j = lane + 64 * u;
-      float sv = -INFINITY;
-      if (j <= pos) {
-        const float* kr = Ks + j * dhp;
-        float a = 0.f;
-        for (int k = 0; k < dh; ++k) a += Qs[k] * kr[k];
-        sv = a * inv_attn_scale;
-      }
-      sc[u] = sv;
-      mx = fmaxf(mx, sv);
-    }
-    mx = wave_max(mx);
-    float sum = 0.f;
-#pragma unroll
-    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-      const float ev = (sc[u] == -INFINITY) ? 0.f : expf(sc[u] - mx);
-      sc[u] = ev;
-      sum += ev;
-    }
-    sum = wave_sum(sum);
-#pragma unroll
-    for (int u = 0; u < ATT_MAX_T / 64; ++u) {
-      const int j = lane + 64 * u;
-      if (j <= pos) Ps[j] = sc[u] / sum;
-    }
-    wave_lds_fence();
-    const size_t zrow = (size_t)(sd.row0 + i);
-    for (int k = lane; k < dh; k += 64) {
-      float a = 0.f;
-      for (int j = 0; j <= pos; ++j) a += Ps[j] * Vs[j * dhp + k];
-      if constexpr (FMT != ACT_F32)
-        store_act<FMT>((uint16_t*)z + zrow * 2 * ldz + h * dh + k, ldz, a, flag);
-      else
-        ((float*)z)[zrow * ldz + h * dh + k] = a;
-      if (zf) zf[zrow * ldzf + h * dh + k] = a;
-    }
-    wave_lds_fence();
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Site entry: materialise resid_pre[e] rows of every site entering at layer e
@@ -412,9 +284,6 @@ __device__ __forceinline__ void stats_merge(float& m, float& s, float om, float 
   s = (m == -INFINITY ? 0.f : s * expf(m - nm)) + (om == -INFINITY ? 0.f : os * expf(om - nm));
   m = nm;
 }
-__device__ __forceinline__ void argmax_merge(float& bv, int& bi, float ov, int oi) {
-  if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-}
 
 __global__ void __launch_bounds__(STATS_THREADS)
 row_stats_kernel(const float* __restrict__ logits, int ldl, int V,
@@ -512,6 +381,57 @@ row_stats_kernel(const float* __restrict__ logits, int ldl, int V,
       out_topk[(size_t)r * topk + j] = fi;
     }
     __syncthreads();
+  }
+}
+
+// Combine the per-tile records of EPI_STATS (gemm_f32.hpp GemmEpi::stats) into
+// each row's target probability and top-k: one wave per row; lane l merges
+// tiles l, l + 64, ... in order, then a butterfly (fixed order: deterministic).
+// Top-k: topk rounds of (value desc, column asc) argmax over every tile's
+// candidates with the chosen columns excluded; each column is a candidate of
+// exactly one tile, and a tile's K candidates include every column of it that
+// can be in the row's top K.
+constexpr int MERGE_WAVES = 4;
+__global__ void __launch_bounds__(64 * MERGE_WAVES)
+stats_merge_kernel(const float* __restrict__ part, int tiles, int K, const float* __restrict__ tlogit,
+                   const int32_t* __restrict__ targets, int n, int V, float* __restrict__ out_prob,
+                   int32_t* __restrict__ out_topk, int topk) {
+  __shared__ int s_sel[MERGE_WAVES][STATS_MAX_K];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * MERGE_WAVES + wave;
+  if (r >= n) return;
+  const int rec = 2 + 2 * K;
+  const float* base = part + (size_t)r * tiles * rec;
+  float m = -INFINITY, s = 0.f;
+  for (int t = lane; t < tiles; t += 64) stats_merge(m, s, base[(size_t)t * rec], base[(size_t)t * rec + 1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    stats_merge(m, s, om, os);
+  }
+  if (out_prob && lane == 0) {
+    const int tg = targets ? targets[r] : -1;
+    out_prob[r] = (tg >= 0 && tg < V) ? expf(tlogit[r] - m) / s : 0.f;
+  }
+  if (!out_topk || topk <= 0) return;
+  for (int j = 0; j < topk; ++j) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t = lane; t < tiles; t += 64) {
+      const float* c = base + (size_t)t * rec + 2;
+      for (int q = 0; q < K; ++q) {
+        const int id = __float_as_int(c[K + q]);
+        bool taken = false;
+        for (int u = 0; u < j; ++u) taken |= s_sel[wave][u] == id;
+        if (!taken) argmax_merge(bv, bi, c[q], id);
+      }
+    }
+    wave_argmax(bv, bi);
+    if (lane == 0) {
+      s_sel[wave][j] = bi;
+      out_topk[(size_t)r * topk + j] = bi;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // s_sel[wave][j] before the next round's reads
   }
 }
 

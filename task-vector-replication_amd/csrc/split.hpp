@@ -19,6 +19,31 @@
 
 namespace tvr {
 
+// Butterfly reductions over one 64-lane wave (fixed order: deterministic).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// (value desc, index asc) argmax merge: torch.argmax's first-occurrence rule
+__device__ __forceinline__ void argmax_merge(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+__device__ __forceinline__ void wave_argmax(float& bv, int& bi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    argmax_merge(bv, bi, ov, oi);
+  }
+}
+
+
 enum ActFmt { ACT_F32 = 0, ACT_X2F16 = 1, ACT_BF16 = 2 };
 
 constexpr float X2_ASCALE = 16.0f;

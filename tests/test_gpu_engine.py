@@ -685,3 +685,43 @@ def test_string_prompt_paths_with_bpe_tokenizer(tiny_cfg, tiny_sd):
     ctx = task[:20]
     assert tvr_amd.check_accuracy_of_task_vector(fv.cuda(), 1, ctx, model=model) == \
         R.check_accuracy_of_task_vector(fv, 1, ctx, model=oracle)
+
+
+@pytest.mark.parametrize("shape", ["tiny", "pythia-160m"])
+@pytest.mark.parametrize("gemm", ["x2f16", "bf16"])
+def test_fused_unembed_statistics_match_logits_path(shape, gemm):
+    """The unembed GEMM's fused statistics epilogue (EPI_STATS: per 256-column
+    tile max / sum exp / top-k candidates / target logit, no logits in HBM) +
+    stats_merge_kernel equals the materialised-logits path (same GEMM, then
+    row_stats_kernel) and torch on those logits: probabilities to 1e-6 of the
+    largest, top-k ids identical for k = 1, 5, 16, on clean prompts and on
+    patch sites.  V = 512 (2 tiles) and 50304 (196 full tiles + one of 128)."""
+    cfg = tvr_amd.get_config(shape)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=1, std=0.1)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", gemm=gemm)
+    prompts = ragged_prompts(37, cfg.d_vocab, 5, lo=2, hi=30)
+    trace = model.trace(len(prompts), sum(map(len, prompts)))
+    with_logits = model.forward_clean(prompts, trace=trace, return_logits=True)["logits"]
+    targets = [int(torch.topk(l, 3).indices[i % 3]) for i, l in enumerate(with_logits)]  # high-probability targets
+    targets[1] = cfg.d_vocab - 1  # the last column of the last (partial) tile
+    for k in (1, 5, 16):
+        fused = model.forward_clean(prompts, targets=targets, topk=k)
+        ref = model.forward_clean(prompts, targets=targets, topk=k, return_logits=True)
+        p = torch.softmax(ref["logits"].double(), -1)
+        assert (fused["prob"].double() - ref["prob"].double()).abs().max().item() <= 1e-6 * p.max().item()
+        assert torch.equal(fused["topk"], ref["topk"])
+        assert fused["topk"].long().tolist() == torch.topk(ref["logits"], k).indices.tolist()
+    g = torch.Generator().manual_seed(2)
+    vecs = (torch.randn(4, cfg.d_model, generator=g) * 2).cuda()
+    sites = tvr_amd.make_sites(len(prompts) * 3)
+    for i in range(len(prompts)):
+        for j, kind in enumerate((tvr_amd._lib.SITE_REPLACE_HEAD_ALLPOS, tvr_amd._lib.SITE_ADD_ATTN_OUT_LASTPOS,
+                                  tvr_amd._lib.SITE_NONE)):
+            s = sites[3 * i + j]
+            s["seq"], s["kind"], s["layer"], s["head"], s["vec"] = i, kind, (i + j) % cfg.n_layers, i % cfg.n_heads, j
+            s["target"] = targets[i]
+    fused = model.patch_sweep(trace, sites, vecs, topk=5)
+    ref = model.patch_sweep(trace, sites, vecs, topk=5, return_logits=True)
+    p = torch.softmax(ref["logits"].double(), -1)
+    assert (fused["prob"].double() - ref["prob"].double()).abs().max().item() <= 1e-6 * p.max().item()
+    assert torch.equal(fused["topk"], ref["topk"])

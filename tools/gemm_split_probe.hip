@@ -20,7 +20,7 @@
 #include <vector>
 
 #include "../task-vector-replication_amd/csrc/gemm_pingpong.hpp"
-#include "../task-vector-replication_amd/csrc/gemm_planar.hpp"
+#include "gemm_planar_probe.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x2f16.hpp"
 #include "../task-vector-replication_amd/csrc/gemm_x3bf16.hpp"
 
