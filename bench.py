@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--shard", default="heads", choices=("heads", "prompts"),
                     help="N>1: heads = C3's site split (strong scaling), prompts = per-GPU prompts (weak scaling)")
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the separate profiled pass")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="N=1 only, planning aid: time rank 0's share of a --shard heads run on this many GPUs "
+                         "(heads = 0 mod G) on this one GPU; value = the units of that share / its time")
     ap.add_argument("--gemm", default="x2f16", choices=("x2f16", "x3bf16", "f32", "bf16"),
                     help="matrix-core path of the GEMMs (x2f16 / x3bf16 / f32 fp32-accurate; bf16 is the "
                          "north star's bf16 configuration, not the fp32 headline)")
@@ -260,10 +263,11 @@ def main():
         mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
 
     shard = args.shard if world > 1 else "heads"
+    emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
     if shard == "heads":  # C3: the same prompts everywhere, sites with head = rank (mod world)
         prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234)
-        heads = strided_shard(cfg.n_heads, rank, world)
-        units_total = len(prompts) * cfg.n_layers * cfg.n_heads
+        heads = strided_shard(cfg.n_heads, rank, emulate or world)
+        units_total = len(prompts) * cfg.n_layers * (len(heads) if emulate else cfg.n_heads)
     else:  # weak scaling: per-rank prompts, every site
         prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
         heads = list(range(cfg.n_heads))
@@ -310,7 +314,11 @@ def main():
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
     T = len(prompts[0])
-    if shard == "heads" and world > 1:
+    if emulate:
+        workload = (f"{args.model} CIE sweep, rank 0's share of a {emulate}-GPU head split ({len(heads)} of "
+                    f"{cfg.n_heads} heads x {cfg.n_layers} layers), {args.prompts} prompts/step, {args.kshot}-shot, "
+                    f"T={len(prompts[0])} (planning emulation on one GPU, not the metric)")
+    elif shard == "heads" and world > 1:
         workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/step, "
                     f"{args.kshot}-shot, T={T}, sites h = rank (mod {world})")
     else:
@@ -395,7 +403,9 @@ def main():
             "max_abs_cie_diff_vs_f32": float((cie - cie32).abs().max()),
             "max_abs_cie": float(cie32.abs().max()),
         }
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if emulate:
+        out["emulated_world"] = emulate
+    if rank == 0 and world == 1 and args.cpu_baseline and not emulate:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -21,7 +21,7 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout", "3": "qkv_mlpin"}
+VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout", "3": "qkv_mlpin", "4": "unembed"}
 SIMDS = 1024  # 256 CUs x 4
 
 
