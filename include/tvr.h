@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 5
+#define TVR_ABI_VERSION 6
 
 enum tvr_status {
   TVR_OK = 0,
@@ -127,7 +127,7 @@ int tvr_model_destroy(tvr_model* model);
  *   TVR_GEMM_X3BF16  fp32-accurate 3-plane bf16 split on v_mfma_f32_32x32x16_bf16:
  *                    each operand x = x0+x1+x2 (bf16 planes, 24 significand bits),
  *                    six cross products accumulated in fp32; weight planes 6 B/param
- *   TVR_GEMM_X2F16   fp32-accurate 2-plane fp16 split on v_mfma_f32_32x32x16_f16
+ *   TVR_GEMM_X2F16   fp32-accurate 2-plane fp16 split on v_mfma_f32_16x16x32_f16
  *                    (the fp16 form of 3xTF32): x = x0+x1 (2 x 11 significand
  *                    bits, power-of-two scaled into fp16 range), three cross
  *                    products accumulated in fp32; weight planes 4 B/param.
@@ -180,6 +180,19 @@ int tvr_forward_clean(tvr_model* model, tvr_trace* trace, const int32_t* tokens,
                       const int32_t* targets, float* out_prob,
                       int32_t* out_topk, int32_t topk, float* out_logits,
                       float* capture_zsum, void* stream);
+
+/* Logits of EVERY position, out_logits device [sum(seq_lens)][V]: the
+ * TransformerLens forward's [1, T, V] (scratch2.py:143,183,297;
+ * scratch.py:127,143).  Exactly one input:
+ *   tokens   host ids (packed, seq_lens per sequence), start_layer 0, or
+ *   resid_in device [sum(seq_lens)][d] = blocks.{start_layer}.hook_resid_pre,
+ *            continued from that block (forward(resid, start_at_layer=L),
+ *            scratch.py:143,206,209).
+ * Sequences up to n_ctx tokens (beyond 128 the attention runs its chunked
+ * online-softmax form). */
+int tvr_forward_logits(tvr_model* model, const int32_t* tokens, const float* resid_in,
+                       int32_t start_layer, const int32_t* seq_lens, int32_t n_seq,
+                       float* out_logits, void* stream);
 
 /* Batched patch sweep over sites against a clean trace (the staircase: a site
  * at layer l reuses the clean run's layers <= l and K/V prefix).  Replaces the

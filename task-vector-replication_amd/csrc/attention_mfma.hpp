@@ -35,21 +35,27 @@ constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 
 // grid = ceil(n_seqs * n_heads / ATTM_WAVES) blocks of 64 * ATTM_WAVES threads;
 // NKT = key tiles the launch's longest sequence needs (1, 2, 4 or 8: the
-// register arrays are sized by it).  Latency-bound (short dependent MFMA
-// chains, global loads): as many waves per SIMD as the fragments allow without
-// spilling (4 at one key tile, 3 up to four, else 2).
+// register arrays are sized by it), or 0 for longer sequences (up to n_ctx):
+// the keys then go in chunks of 8 tiles with an online softmax (running max
+// and sum per query, the z accumulator rescaled per chunk) and key tiles past
+// the query tile's last position are skipped.  Latency-bound (short dependent
+// MFMA chains, global loads): as many waves per SIMD as the fragments allow
+// without spilling (4 at one key tile, 3 up to four, else 2).
+// zf_last: the fp32 hook_z copy only for each sequence's last row, at row s of
+// zf (the extraction's capture reads nothing else), instead of every row.
 template <int FMT, int DH, int NKT>
-__global__ void __launch_bounds__(64 * ATTM_WAVES, (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4) ? 3 : 2)
+__global__ void __launch_bounds__(64 * ATTM_WAVES, (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
 attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
                       const SeqDesc* __restrict__ seqs, int n_seqs, int n_heads, void* __restrict__ z, int ldz,
-                      float* __restrict__ zf, int ldzf, unsigned* __restrict__ flag,
+                      float* __restrict__ zf, int ldzf, int zf_last, unsigned* __restrict__ flag,
                       const float* __restrict__ cos_t, const float* __restrict__ sin_t, int d,
                       float inv_attn_scale) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int CH = DH / 4;    // dims per lane group in Q K^T
   constexpr int NDT = DH / 16;  // 16-dim output tiles
-  constexpr int MAXKT = NKT;
-  static_assert(DH % 16 == 0 && DH <= 128 && NKT * 16 <= ATT_MAX_T, "d_head / key tiles");
+  constexpr bool LONG = NKT == 0;
+  constexpr int MAXKT = LONG ? 8 : NKT;
+  static_assert(DH % 16 == 0 && DH <= 128 && MAXKT * 16 <= ATT_MAX_T, "d_head / key tiles");
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
   if (pair >= n_seqs * n_heads) return;  // a whole wave; nothing below synchronises
@@ -92,93 +98,172 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     const int qi = min(q0 + li, sd.n - 1);
     float qf[CH];
     load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
-    // one key tile (T <= 16, the C3 sweeps): V's fragments are loaded with Q and
-    // K, so the wave pays one global-memory latency instead of two
-    constexpr int VP = NKT == 1 ? 4 : 1, VPD = NKT == 1 ? NDT : 1;
-    float vpre[VP][VPD];
-    if constexpr (NKT == 1) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float* vr = row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
-      }
-    }
-
-    f4 st[MAXKT];
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-      st[kt] = f4{0.f, 0.f, 0.f, 0.f};
-      if (kt < nkt) {
-        const int kj = min(16 * kt + li, T - 1);
-        float kf[CH];
-        load_chunk(row_of(kj) + d + h * DH, kj, kf);
-        // two accumulation chains (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
-        f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < CH; c += 2) {
-          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c], qf[c], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c + 1], qf[c + 1], a1, 0, 0, 0);
-        }
-        st[kt] = a0 + a1;
-      }
-      // one key tile's fragments live at a time (hoisting every tile's loads spills)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // causal softmax over keys 16kt + 4g + r for the query at absolute position qpos
-    const int qpos = sd.p0 + q0 + li;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = 16 * kt + 4 * g + r;
-        const float v = (kt < nkt && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
-        st[kt][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - mx);
-        st[kt][r] = e;
-        sum += e;
-      }
-    }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) st[kt][r] = st[kt][r] / sum;
-    }
-
     f4 zt[NDT];
+    if constexpr (LONG) {
+      const int qpos = sd.p0 + q0 + li;  // this lane's query (absolute position)
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
+      // running max / sum of this lane's query over the chunks of keys so far
+      float m_run = -INFINITY, l_run = 0.f;
+      // key tiles this query tile sees (causal): through its last row's position
+      const int kt_end = min(nkt, (sd.p0 + min(q0 + 15, sd.n - 1)) / 16 + 1);
+      for (int kb = 0; kb < kt_end; kb += MAXKT) {
+        f4 st[MAXKT];
 #pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-      if (kt < nkt) {
+        for (int kt = 0; kt < MAXKT; ++kt) {
+          st[kt] = f4{0.f, 0.f, 0.f, 0.f};
+          if (kb + kt < kt_end) {
+            const int kj = min(16 * (kb + kt) + li, T - 1);
+            float kf[CH];
+            load_chunk(row_of(kj) + d + h * DH, kj, kf);
+            f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if constexpr (NKT == 1) {
+            for (int c = 0; c < CH; c += 2) {
+              a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c], qf[c], a0, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c + 1], qf[c + 1], a1, 0, 0, 0);
+            }
+            st[kt] = a0 + a1;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        float mx = -INFINITY;
 #pragma unroll
-            for (int dt = 0; dt < NDT; ++dt)
-              zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vpre[r][dt], st[kt][r], zt[dt], 0, 0, 0);
-          } else {
-            const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+        for (int kt = 0; kt < MAXKT; ++kt) {
 #pragma unroll
-            for (int dt = 0; dt < NDT; ++dt)
-              zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+          for (int r = 0; r < 4; ++r) {
+            const int key = 16 * (kb + kt) + 4 * g + r;
+            const float v = (kb + kt < kt_end && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
+            st[kt][r] = v;
+            mx = fmaxf(mx, v);
           }
         }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        // online softmax: rescale what the earlier chunks accumulated (key 0 is in
+        // the first chunk of every query, so m_new is finite from there on)
+        const float m_new = fmaxf(m_run, mx);
+        const float scale = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+        m_run = m_new;
+        float sum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - m_new);
+            st[kt][r] = e;
+            sum += e;
+          }
+        }
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        l_run = l_run * scale + sum;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) zt[dt] *= scale;
+#pragma unroll
+        for (int kt = 0; kt < MAXKT; ++kt) {
+          if (kb + kt < kt_end) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float* vr = row_of(min(16 * (kb + kt) + 4 * g + r, T - 1)) + 2 * d + h * DH + li;
+#pragma unroll
+              for (int dt = 0; dt < NDT; ++dt)
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      __builtin_amdgcn_sched_barrier(0);
+      // zt[dt]: dims of query li (D[dim][query li]); l_run is that query's softmax sum
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) zt[dt] /= l_run;
+    } else {
+      // one key tile (T <= 16, the C3 sweeps): V's fragments are loaded with Q and
+      // K, so the wave pays one global-memory latency instead of two
+      constexpr int VP = NKT == 1 ? 4 : 1, VPD = NKT == 1 ? NDT : 1;
+      float vpre[VP][VPD];
+      if constexpr (NKT == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* vr = row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
+        }
+      }
+
+      f4 st[MAXKT];
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt) {
+        st[kt] = f4{0.f, 0.f, 0.f, 0.f};
+        if (kt < nkt) {
+          const int kj = min(16 * kt + li, T - 1);
+          float kf[CH];
+          load_chunk(row_of(kj) + d + h * DH, kj, kf);
+          // two accumulation chains (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
+          f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < CH; c += 2) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c], qf[c], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c + 1], qf[c + 1], a1, 0, 0, 0);
+          }
+          st[kt] = a0 + a1;
+        }
+        // one key tile's fragments live at a time (hoisting every tile's loads spills)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // causal softmax over keys 16kt + 4g + r for the query at absolute position qpos
+      const int qpos = sd.p0 + q0 + li;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * kt + 4 * g + r;
+          const float v = (kt < nkt && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
+          st[kt][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = st[kt][r] == -INFINITY ? 0.f : expf(st[kt][r] - mx);
+          st[kt][r] = e;
+          sum += e;
+        }
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[kt][r] = st[kt][r] / sum;
+      }
+
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt) {
+        if (kt < nkt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if constexpr (NKT == 1) {
+#pragma unroll
+              for (int dt = 0; dt < NDT; ++dt)
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vpre[r][dt], st[kt][r], zt[dt], 0, 0, 0);
+            } else {
+              const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+#pragma unroll
+              for (int dt = 0; dt < NDT; ++dt)
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     if (q0 + li < sd.n) {
       const size_t zrow = (size_t)(sd.row0 + q0 + li);
@@ -190,7 +275,8 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
           store_act4<FMT>((uint16_t*)z + zrow * 2 * ldz + col, ldz, v[0], v[1], v[2], v[3], flag);
         else
           *(f4*)((float*)z + zrow * ldz + col) = v;
-        if (zf) *(f4*)(zf + zrow * ldzf + col) = v;
+        if (zf && !zf_last) *(f4*)(zf + zrow * ldzf + col) = v;
+        if (zf && zf_last && q0 + li == sd.n - 1) *(f4*)(zf + (size_t)s * ldzf + col) = v;
       }
     }
   }

@@ -515,7 +515,7 @@ struct Acts {
 // the Pythia head sizes d_head 16 (tiny), 64, 80, 128 with rotary_dim =
 // d_head / 4 (every Pythia: rotary_pct 0.25); check_config rejects the rest.
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
-                     int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st) {
+                     int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st, bool zf_last = false) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
@@ -523,15 +523,18 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const int dh = c.d_head;
   const int pairs = n_seqs * c.n_heads;
   const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
-  const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : 8;
+  // key tiles in registers: 1 / 2 / 4 / 8, or 0 = longer than 128 (chunked online softmax)
+  const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 0;
 #define TVR_ATTM(F, DHV, NK)                                                                                        \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
-                     n_seqs, c.n_heads, z, m->K2, zf, d, m->range_flag, m->rot_cos, m->rot_sin, d, inv_scale)
+                     n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, m->range_flag, m->rot_cos, m->rot_sin, d, \
+                     inv_scale)
 #define TVR_ATTM_NK(F, DHV)                                                                     \
   if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                            \
   else if (nkt == 2) TVR_ATTM(F, DHV, 2);                                                       \
   else if (nkt == 4) TVR_ATTM(F, DHV, 4);                                                       \
-  else TVR_ATTM(F, DHV, 8)
+  else if (nkt == 8) TVR_ATTM(F, DHV, 8);                                                       \
+  else TVR_ATTM(F, DHV, 0)
 #define TVR_ATTM_DH(F)                                                                          \
   if (dh == 16) { TVR_ATTM_NK(F, 16); } else if (dh == 64) { TVR_ATTM_NK(F, 64); }              \
   else if (dh == 80) { TVR_ATTM_NK(F, 80); } else { TVR_ATTM_NK(F, 128); }
@@ -578,13 +581,14 @@ GemmEpi epi_qkv_mlpin(tvr_model* m, const float* b1, float* qkv, const Acts& a) 
 // every row of the launch (fp32 qkv), z out in the activation format, plus the
 // fp32 hook_z copy when one is written (trace / capture).  The shared prefix
 // rows read from the trace or a leader are not counted.
-double attention_bytes(int d, int q_rows, int kv_rows, int fmt, bool zf) {
-  return ((double)q_rows * d + 2.0 * kv_rows * d) * 4.0 +
-         (double)q_rows * d * ((fmt == ACT_BF16 ? 2.0 : 4.0) + (zf ? 4.0 : 0.0));
+double attention_bytes(int d, int q_rows, int kv_rows, int fmt, int zf_rows) {
+  return ((double)q_rows * d + 2.0 * kv_rows * d) * 4.0 + (double)q_rows * d * (fmt == ACT_BF16 ? 2.0 : 4.0) +
+         (double)zf_rows * d * 4.0;
 }
 
+// zf_last: the fp32 hook_z copy of each sequence's last row only, at row s of zf
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
-              Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st) {
+              Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st, bool zf_last = false) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -593,8 +597,8 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, R, m->D1, d,
                       e1, st, m));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st));
-  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf != nullptr));
+  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf ? (zf_last ? n_seqs : R) : 0));
   return TVR_OK;
 }
 
@@ -606,7 +610,7 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
 // (nothing downstream reads the final residual).
 int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT, Acts& a,
                         const float* cache_qkv, const int32_t* d_last, int n_last, bool write_out,
-                        float* zf, hipStream_t st) {
+                        float* zf, hipStream_t st, bool zf_last = false) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -624,8 +628,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, n_last, m->D1,
                       d, e1, st, m));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st));
-  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf != nullptr));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? n_last : 0));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
   e2.bias = w.b2;
@@ -1005,11 +1009,22 @@ int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, 
 
 int32_t tvr_trace_num_tokens(const tvr_trace* t) { return t ? t->n_tokens : 0; }
 
-int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const int32_t* seq_lens,
-                      int32_t n_seq, const int32_t* targets, float* out_prob, int32_t* out_topk,
-                      int32_t topk, float* out_logits, float* capture_zsum, void* stream) {
-  if (!m || !tokens || !seq_lens || n_seq <= 0)
+}  // extern "C"
+
+namespace {
+// The batched clean forward behind tvr_forward_clean / tvr_forward_logits.
+//   tokens     host ids (embedded), or nullptr with resid_in: device [R][d]
+//              hook_resid_pre of start_layer (TL forward(resid, start_at_layer=))
+//   all_rows   logits of EVERY row to out_logits [R][V] (TL forward's [1, T, V]);
+//              otherwise each sequence's last row (out_prob / out_topk / out_logits [n][V])
+int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const float* resid_in, int start_layer,
+                 const int32_t* seq_lens, int32_t n_seq, const int32_t* targets, float* out_prob,
+                 int32_t* out_topk, int32_t topk, float* out_logits, bool all_rows, float* capture_zsum,
+                 void* stream) {
+  if (!m || (!tokens && !resid_in) || !seq_lens || n_seq <= 0)
     return fail(TVR_ERR_INVALID, "tvr_forward_clean: bad argument");
+  if (start_layer < 0 || start_layer >= m->cfg.n_layers || (tokens && start_layer != 0) || (resid_in && trace))
+    return fail(TVR_ERR_INVALID, "forward: start_layer needs a residual input and no trace");
   if (topk < 0 || topk > STATS_MAX_K) return fail(TVR_ERR_INVALID, "topk must be in [0, 16]");
   if (topk > 0 && !out_topk) return fail(TVR_ERR_INVALID, "topk > 0 needs out_topk");
   hipStream_t st = (hipStream_t)stream;
@@ -1020,15 +1035,15 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   for (int s = 0; s < n_seq; ++s) {
     const int T = seq_lens[s];
     if (T <= 0) return fail(TVR_ERR_INVALID, "sequence " + std::to_string(s) + " is empty");
-    if (T > ATT_MAX_T || T > c.n_ctx)
-      return fail(TVR_ERR_UNSUPPORTED, "sequence length " + std::to_string(T) + " exceeds " +
-                                           std::to_string(std::min(ATT_MAX_T, c.n_ctx)));
+    if (T > c.n_ctx)
+      return fail(TVR_ERR_UNSUPPORTED, "sequence length " + std::to_string(T) + " exceeds n_ctx " +
+                                           std::to_string(c.n_ctx));
     off[s] = R;
     last[s] = R + T - 1;
     R += T;
     maxT = std::max(maxT, T);
   }
-  for (int r = 0; r < R; ++r)
+  for (int r = 0; tokens && r < R; ++r)
     if (tokens[r] < 0 || tokens[r] >= c.d_vocab)
       return fail(TVR_ERR_INVALID, "token id " + std::to_string(tokens[r]) + " out of range");
   if (trace && (n_seq > trace->max_seqs || R > trace->max_tokens))
@@ -1036,14 +1051,14 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
 
   std::vector<SeqDesc> seqs(n_seq);
   for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1, 0, 0};
-  std::vector<int32_t> tok(tokens, tokens + R);
+  std::vector<int32_t> tok = tokens ? std::vector<int32_t>(tokens, tokens + R) : std::vector<int32_t>();
   // Shared prefixes without a trace (only each prompt's last row is read
   // afterwards): a prompt whose leading tokens equal those of the first prompt
   // with its first token computes only the rows after the common prefix and
   // reads the prefix K/V from that prompt's rows (SeqDesc.prefix_live); every
   // extraction prompt starts with BOS.  With a trace every row is kept (patch
   // sweeps read any position of it).
-  if (!trace && prefix_share_enabled()) {
+  if (!trace && tokens && !all_rows && prefix_share_enabled()) {
     std::map<int, int> first;  // first token -> first prompt starting with it
     std::vector<int32_t> ctok;
     ctok.reserve(R);
@@ -1070,18 +1085,25 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
     R = Rc;
   }
   // without a trace only each prompt's last row is read after the last layer
-  const bool trim = trace == nullptr;
+  const bool trim = trace == nullptr && !all_rows;
   std::vector<SeqDesc> seqs_last(seqs);
   for (auto& q : seqs_last) q.q0 = q.n - 1;
   std::vector<int32_t> tg(n_seq, -1);
   if (targets) std::copy(targets, targets + n_seq, tg.begin());
 
-  const int FC = std::min(kFinalChunk, n_seq);
+  const int n_out = all_rows ? R : n_seq;  // rows of the final LN + unembed
+  std::vector<int32_t> out_rows;
+  if (all_rows) {
+    out_rows.resize(R);
+    for (int r = 0; r < R; ++r) out_rows[r] = r;
+  }
+  const int FC = std::min(kFinalChunk, n_out);
   Carve cv;
   const size_t o_seqs = cv.take<SeqDesc>(n_seq);
   const size_t o_seqs_last = cv.take<SeqDesc>(n_seq);
   const size_t o_tok = cv.take<int32_t>(R);
   const size_t o_last = cv.take<int32_t>(n_seq);
+  const size_t o_rows = all_rows ? cv.take<int32_t>(R) : 0;
   const size_t o_tg = cv.take<int32_t>(n_seq);
   const size_t o_resid = cv.take<float>((size_t)R * d);
   const size_t o_xn = cv.take<float>((size_t)R * d);
@@ -1090,8 +1112,10 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   const size_t o_xf = cv.take<float>((size_t)FC * d);
   const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, topk, out_logits));
   const size_t o_cap = capture_zsum ? cv.take<float>((size_t)CAP_GROUPS * d) : 0;
-  // fp32 hook_z for the capture when no trace slot receives it
-  const size_t o_zf = (capture_zsum && !trace) ? cv.take<float>((size_t)R * d) : 0;
+  // fp32 hook_z of each prompt's last row for the capture when no trace slot
+  // receives it (the attention kernel writes that row only, at row s)
+  const bool zf_last = capture_zsum && !trace;
+  const size_t o_zf = zf_last ? cv.take<float>((size_t)n_seq * d) : 0;
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -1099,6 +1123,7 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   ub.add(o_seqs_last, seqs_last);
   ub.add(o_tok, tok);
   ub.add(o_last, last);
+  if (all_rows) ub.add(o_rows, out_rows);
   ub.add(o_tg, tg);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
@@ -1109,14 +1134,16 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
   const int32_t* d_last = (const int32_t*)(base + o_last);
   const size_t tstride = trace ? (size_t)trace->max_tokens * d : 0;
 
-  {
+  if (tokens) {
     const size_t total = (size_t)R * (d / 4);
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(embed_kernel, dim3(blocks), dim3(256), 0, st, (const int32_t*)(base + o_tok),
                        m->w_embed, a.resid, R, d);
     TVR_HIP(hipGetLastError());
+  } else {
+    TVR_HIP(hipMemcpyAsync(a.resid, resid_in, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
-  for (int l = 0; l < L; ++l) {
+  for (int l = start_layer; l < L; ++l) {
     if (trace)
       TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, (size_t)R * d * sizeof(float),
                              hipMemcpyDeviceToDevice, st));
@@ -1126,15 +1153,15 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
     const bool want_out = out_prob || out_topk || out_logits;
     if (trim && l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, R, (const SeqDesc*)(base + o_seqs_last), n_seq, maxT, a, nullptr,
-                                  d_last, n_seq, want_out, zf, st));
+                                  d_last, n_seq, want_out, zf, st, zf_last));
     } else {
-      TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, zf, st));
+      TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, zf, st, zf_last));
     }
     if (capture_zsum) {
       float* part = (float*)(base + o_cap);
       ProfSpan ps(m, st);
       hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
-                         zf, d, d_last, n_seq, part, d);
+                         zf, d, zf_last ? nullptr : d_last, n_seq, part, d);
       hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part,
                          capture_zsum + (size_t)l * d, d);
       TVR_HIP(hipGetLastError());
@@ -1147,15 +1174,39 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
                            hipMemcpyDeviceToDevice, st));
     trace->seq_off.assign(off.begin(), off.end());
     trace->seq_len.assign(seq_lens, seq_lens + n_seq);
-    trace->tokens.assign(tokens, tokens + R);
+    trace->tokens.assign(tokens, tokens + R);  // trace => tokens (checked above)
     trace->n_seq = n_seq;
     trace->n_tokens = R;
   }
-  if (out_prob || out_topk || out_logits)
+  if (all_rows)
+    TVR_TRY(run_final(m, a.resid, (const int32_t*)(base + o_rows), nullptr, R, (float*)(base + o_xf),
+                      (float*)(base + o_lg), nullptr, nullptr, 0, out_logits, fmt, st));
+  else if (out_prob || out_topk || out_logits)
     TVR_TRY(run_final(m, a.resid, d_last, (const int32_t*)(base + o_tg), n_seq, (float*)(base + o_xf),
                       (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st));
   return TVR_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const int32_t* seq_lens,
+                      int32_t n_seq, const int32_t* targets, float* out_prob, int32_t* out_topk,
+                      int32_t topk, float* out_logits, float* capture_zsum, void* stream) {
+  if (!tokens) return fail(TVR_ERR_INVALID, "tvr_forward_clean: bad argument");
+  return forward_impl(m, trace, tokens, nullptr, 0, seq_lens, n_seq, targets, out_prob, out_topk, topk, out_logits,
+                      false, capture_zsum, stream);
+}
+
+int tvr_forward_logits(tvr_model* m, const int32_t* tokens, const float* resid_in, int32_t start_layer,
+                       const int32_t* seq_lens, int32_t n_seq, float* out_logits, void* stream) {
+  if (!out_logits || (tokens == nullptr) == (resid_in == nullptr))
+    return fail(TVR_ERR_INVALID, "tvr_forward_logits: give exactly one of tokens / resid_in, and out_logits");
+  return forward_impl(m, nullptr, tokens, resid_in, start_layer, seq_lens, n_seq, nullptr, nullptr, nullptr, 0,
+                      out_logits, true, nullptr, stream);
+}
+
+
 
 int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites, int32_t n_sites,
                     const float* vectors, int32_t n_vectors, float* out_prob, int32_t* out_topk,
@@ -1347,7 +1398,7 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
     const float* snap = trace->resid + (size_t)l * tstride;
     const float* zsnap = l > 0 ? trace->z + (size_t)(l - 1) * tstride : nullptr;
     const float* w2 = l > 0 ? m->layers[l - 1].w2 : nullptr;
-    const size_t zbytes = (size_t)maxT * c.d_head * sizeof(float);
+    const size_t zbytes = (size_t)std::min(maxT, ENTRY_LDS_POS) * c.d_head * sizeof(float);
     if (zbytes > 64 * 1024)
       TVR_HIP(hipFuncSetAttribute((const void*)entry_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)zbytes));

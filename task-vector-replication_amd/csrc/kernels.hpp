@@ -155,7 +155,9 @@ constexpr int ENTRY_THREADS = 256;
 constexpr int ENTRY_POS_CHUNK = 16;
 constexpr int ENTRY_K_CHUNK = 16;
 
-// dynamic LDS: T x dh floats (the site's head slice of z; REPLACE_HEAD only)
+// dynamic LDS: min(T, ENTRY_LDS_POS) x dh floats (the site's head slice of z,
+// staged ENTRY_LDS_POS positions at a time; REPLACE_HEAD only)
+constexpr int ENTRY_LDS_POS = 128;
 __global__ void __launch_bounds__(ENTRY_THREADS)
 entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
              const float* __restrict__ zsnap, const float* __restrict__ w2, int ldw2,
@@ -164,39 +166,44 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
   const EntryDesc e = ents[blockIdx.x];
   const int c = blockIdx.y * ENTRY_THREADS + threadIdx.x;
   if (e.kind == 1) {  // TVR_SITE_REPLACE_HEAD_ALLPOS
-    for (int x = threadIdx.x; x < e.n * dh; x += ENTRY_THREADS) {
-      const int pos = x / dh, k = x - pos * dh;
-      zs[x] = zsnap[(size_t)(e.src_row + e.p0 + pos) * d + e.head * dh + k];
-    }
-    __syncthreads();
-    if (c >= d) return;
-    const float* w = w2 + (size_t)c * ldw2 + e.head * dh;
-    const float vc = vectors[(size_t)e.vec * d + c];
-    for (int p0 = 0; p0 < e.n; p0 += ENTRY_POS_CHUNK) {
-      float acc[ENTRY_POS_CHUNK];
+    const bool col = c < d;  // no early return: every thread joins the barriers
+    const float* w = w2 + (size_t)(col ? c : 0) * ldw2 + e.head * dh;
+    const float vc = col ? vectors[(size_t)e.vec * d + c] : 0.f;
+    for (int s0 = 0; s0 < e.n; s0 += ENTRY_LDS_POS) {
+      const int sn = min(ENTRY_LDS_POS, e.n - s0);
+      __syncthreads();  // the previous chunk's reads are done
+      for (int x = threadIdx.x; x < sn * dh; x += ENTRY_THREADS) {
+        const int pos = x / dh, k = x - pos * dh;
+        zs[x] = zsnap[(size_t)(e.src_row + e.p0 + s0 + pos) * d + e.head * dh + k];
+      }
+      __syncthreads();
+      if (!col) continue;
+      for (int p0 = 0; p0 < sn; p0 += ENTRY_POS_CHUNK) {
+        float acc[ENTRY_POS_CHUNK];
 #pragma unroll
-      for (int u = 0; u < ENTRY_POS_CHUNK; ++u) acc[u] = 0.f;
-      for (int k0 = 0; k0 < dh; k0 += ENTRY_K_CHUNK) {
-        float wk[ENTRY_K_CHUNK];
+        for (int u = 0; u < ENTRY_POS_CHUNK; ++u) acc[u] = 0.f;
+        for (int k0 = 0; k0 < dh; k0 += ENTRY_K_CHUNK) {
+          float wk[ENTRY_K_CHUNK];
 #pragma unroll
-        for (int q = 0; q < ENTRY_K_CHUNK; q += 4) {
-          const float4 v4 = *(const float4*)(w + k0 + q);  // dh % 16 == 0 (checked on the host)
-          wk[q] = v4.x; wk[q + 1] = v4.y; wk[q + 2] = v4.z; wk[q + 3] = v4.w;
+          for (int q = 0; q < ENTRY_K_CHUNK; q += 4) {
+            const float4 v4 = *(const float4*)(w + k0 + q);  // dh % 16 == 0 (checked on the host)
+            wk[q] = v4.x; wk[q + 1] = v4.y; wk[q + 2] = v4.z; wk[q + 3] = v4.w;
+          }
+#pragma unroll
+          for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
+            if (p0 + u < sn) {
+              const float* zr = zs + (p0 + u) * dh + k0;
+#pragma unroll
+              for (int q = 0; q < ENTRY_K_CHUNK; ++q) acc[u] += zr[q] * wk[q];
+            }
+          }
         }
 #pragma unroll
         for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
-          if (p0 + u < e.n) {
-            const float* zr = zs + (p0 + u) * dh + k0;
-#pragma unroll
-            for (int q = 0; q < ENTRY_K_CHUNK; ++q) acc[u] += zr[q] * wk[q];
+          if (p0 + u < sn) {
+            const int i = s0 + p0 + u, pos = e.p0 + i;
+            resid[(size_t)(e.row0 + i) * d + c] = snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
           }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
-        if (p0 + u < e.n) {
-          const int pos = e.p0 + p0 + u;
-          resid[(size_t)(e.row0 + p0 + u) * d + c] = snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
         }
       }
     }
@@ -221,7 +228,8 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
 // ---------------------------------------------------------------------------
 // Capture + mean-over-prompts reduction, z form (mean_p result =
 // (mean_p z) @ W_O).  Deterministic two-pass: partial[g][c] = sum over rows
-// g, g+G, ...; then zsum[c] += sum_g partial[g][c].
+// g, g+G, ...; then zsum[c] += sum_g partial[g][c].  rows == nullptr: row i is
+// z row i (the attention kernel's compact last-row copy).
 constexpr int CAP_GROUPS = 128;  // row groups of the partial pass (fixed-order sums: deterministic)
 __global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
                                        const int32_t* __restrict__ rows, int n,
@@ -234,14 +242,17 @@ __global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
   for (; i + 3 * CAP_GROUPS < n; i += 4 * CAP_GROUPS) {  // four rows' loads in flight, summed in row order
     float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = ((const float4*)(z + (size_t)rows[i + u * CAP_GROUPS] * ldz))[c4];
+    for (int u = 0; u < 4; ++u) {
+      const int r = i + u * CAP_GROUPS;
+      v[u] = ((const float4*)(z + (size_t)(rows ? rows[r] : r) * ldz))[c4];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
     }
   }
   for (; i < n; i += CAP_GROUPS) {
-    const float4 v = ((const float4*)(z + (size_t)rows[i] * ldz))[c4];
+    const float4 v = ((const float4*)(z + (size_t)(rows ? rows[i] : i) * ldz))[c4];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
   ((float4*)(partial + (size_t)g * d))[c4] = s;

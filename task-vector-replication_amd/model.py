@@ -320,10 +320,40 @@ class Model(TokenizerMixin):
             return [int(x) for x in tokens.tolist()]
         return [int(x) for x in tokens]
 
-    def forward(self, tokens) -> torch.Tensor:
-        """Logits of the LAST position, shaped [1, 1, V] (the reference only
-        ever reads ``logits[0, -1]``: scratch2.py:43,112,144,184,192,280)."""
-        out = self.forward_clean([self._as_ids(tokens)], return_logits=True)
-        return out["logits"].view(1, 1, -1)
+    def forward(self, tokens, start_at_layer: Optional[int] = None, last_only: bool = False) -> torch.Tensor:
+        """TransformerLens ``HookedTransformer.forward`` (scratch2.py:143,183,297;
+        scratch.py:127,143,206,209) for batch 1: ``tokens`` (a string, ids [T]
+        or [1, T]) -> logits [1, T, V] of every position; with
+        ``start_at_layer=L``, ``tokens`` is the residual ``hook_resid_pre`` of
+        block L ([1, T, d] or [T, d]) and the forward continues from there.
+        ``last_only`` returns [1, 1, V] (the only row the reference reads)
+        without the other rows' unembedding.  Up to n_ctx tokens."""
+        dev, V = self.device, self.cfg.d_vocab
+        if start_at_layer is None:
+            ids = self._as_ids(tokens)
+            if last_only:
+                return self.forward_clean([ids], return_logits=True)["logits"].view(1, 1, -1)
+            toks, lens = self._pack([ids])
+            out = torch.empty(len(ids), V, device=dev)
+            rc = self._lib.tvr_forward_logits(self._h, toks.ctypes.data, None, 0, lens.ctypes.data, 1,
+                                              out.data_ptr(), self._stream())
+        else:
+            resid = torch.as_tensor(tokens).to(dev, torch.float32)
+            if resid.dim() == 3:
+                if resid.shape[0] != 1:
+                    raise ValueError("batch size must be 1")
+                resid = resid[0]
+            if resid.dim() != 2 or resid.shape[1] != self.cfg.d_model:
+                raise ValueError("start_at_layer needs a residual of shape [1, T, d_model]")
+            resid = resid.contiguous()
+            lens = np.asarray([resid.shape[0]], dtype=np.int32)
+            out = torch.empty(resid.shape[0], V, device=dev)
+            rc = self._lib.tvr_forward_logits(self._h, None, resid.data_ptr(), int(start_at_layer), lens.ctypes.data,
+                                              1, out.data_ptr(), self._stream())
+        _lib.check(rc, "tvr_forward_logits")
+        self._check_range("tvr_forward_logits")
+        if last_only:
+            out = out[-1:]
+        return out.view(1, out.shape[0], V)
 
     __call__ = forward

@@ -275,8 +275,8 @@ def test_forward_rejects_bad_input(tiny_model):
         tiny_model.forward_clean([[0, 1], []])
     with pytest.raises(ValueError):
         tiny_model.forward_clean([[0, tiny_model.cfg.d_vocab]])
-    with pytest.raises(RuntimeError):
-        tiny_model.forward_clean([[0] * 129])
+    with pytest.raises(RuntimeError):  # longer than the model's n_ctx (256 for "tiny")
+        tiny_model.forward_clean([[0] * 257])
 
 
 # --------------------------------------------------------------- experiments
@@ -725,3 +725,77 @@ def test_fused_unembed_statistics_match_logits_path(shape, gemm):
     p = torch.softmax(ref["logits"].double(), -1)
     assert (fused["prob"].double() - ref["prob"].double()).abs().max().item() <= 1e-6 * p.max().item()
     assert torch.equal(fused["topk"], ref["topk"])
+
+
+def test_forward_all_positions_and_start_at_layer(tiny_model, tiny_oracle):
+    """Model.forward is TransformerLens' forward: [1, T, V] logits of every
+    position (scratch2.py:143,183,297) and forward(resid, start_at_layer=L)
+    (scratch.py:143,206,209), through tvr_forward_logits."""
+    rng = random.Random(41)
+    ids = [0] + [rng.randrange(1, tiny_model.cfg.d_vocab) for _ in range(20)]
+    ref = tiny_oracle.forward(torch.tensor([ids]))
+    out = tiny_model.forward(ids)
+    assert out.shape == ref.shape
+    assert rel_err(out[0], ref[0]) < 1e-4
+    assert rel_err(tiny_model.forward(torch.tensor([ids]), last_only=True)[0, 0], ref[0, -1]) < 1e-4
+    assert torch.equal(tiny_model(ids).argmax(-1).cpu(), ref.argmax(-1))
+    _, cache = tiny_oracle.run_with_cache(torch.tensor([ids]))
+    for layer in range(tiny_oracle.cfg.n_layers):
+        resid = cache[f"blocks.{layer}.hook_resid_pre"].clone()
+        resid[0, 5] = cache[f"blocks.{layer}.hook_resid_pre"][0, 9]  # scratch.py:141-142 style surgery
+        want = tiny_oracle.forward(resid, start_at_layer=layer)
+        got = tiny_model.forward(resid.cuda(), start_at_layer=layer)
+        assert rel_err(got[0], want[0]) < 1e-4, layer
+
+
+def test_sequences_longer_than_128(tiny_cfg, tiny_sd, tokenizer):
+    """Prompts past 128 tokens (TransformerLens n_ctx 2048): the attention
+    kernel's chunked online-softmax form, the chunked entry staging and the
+    compact last-row z capture, against the oracle: last-row and all-position
+    logits, extraction sums, every site kind on a 300-token prompt."""
+    from conftest import make_oracle
+    cfg = tiny_cfg.with_(n_ctx=2048)
+    oracle = make_oracle(cfg, tiny_sd, tokenizer)
+    rng = random.Random(43)
+    prompts = [[0] + [rng.randrange(1, cfg.d_vocab) for _ in range(n - 1)] for n in (300, 17, 700, 129, 150)]
+    for gemm in ("x2f16", "f32"):
+        model = tvr_amd.Model.from_hf_state_dict(cfg, tiny_sd, device="cuda", tokenizer=tokenizer, gemm=gemm)
+        out = model.forward_clean(prompts, targets=[p[3] for p in prompts], topk=3, return_logits=True, capture=True)
+        zsum = torch.zeros(cfg.n_layers, cfg.d_model, dtype=torch.float64)
+        for i, p in enumerate(prompts):
+            logits, cache = oracle.run_with_cache(torch.tensor([p]))
+            assert rel_err(out["logits"][i], logits[0, -1]) < 1e-4, (gemm, i)
+            assert out["topk"][i].tolist() == torch.topk(logits[0, -1], 3).indices.tolist()
+            for l in range(cfg.n_layers):
+                zsum[l] += cache[f"blocks.{l}.attn.hook_z"][0, -1].reshape(-1).double()
+        assert rel_err(out["zsum"], zsum) < 1e-4
+        assert rel_err(model.forward(prompts[2])[0], oracle.forward(torch.tensor([prompts[2]]))[0]) < 1e-4
+        # patch sites on the 300-token prompt
+        p = prompts[0]
+        trace = model.trace(len(prompts), sum(map(len, prompts)))
+        model.forward_clean(prompts, trace=trace)
+        vecs = torch.randn(2, cfg.d_model, generator=torch.Generator().manual_seed(7))
+        sites = tvr_amd.make_sites(3)
+        sites[0]["kind"], sites[0]["layer"], sites[0]["head"], sites[0]["vec"] = 1, 0, 2, 0
+        sites[1]["kind"], sites[1]["layer"], sites[1]["vec"] = 2, 1, 1
+        sites[2]["kind"], sites[2]["layer"], sites[2]["pos"], sites[2]["src_seq"], sites[2]["src_pos"] = 3, 1, 100, 2, 600
+        sites["seq"] = 0
+        got = model.patch_sweep(trace, sites, vecs.cuda(), return_logits=True, want_prob=False)["logits"]
+        oracle.cfg.use_attn_result = True
+        try:
+            def rep(hv, hook):
+                hv[0, :, 2, :] = vecs[0]
+                return hv
+            w0 = oracle.run_with_hooks(torch.tensor([p]), fwd_hooks=[("blocks.0.attn.hook_result", rep)])[0, -1]
+        finally:
+            oracle.cfg.use_attn_result = False
+        w1 = oracle.run_with_hooks(torch.tensor([p]), fwd_hooks=[
+            ("blocks.1.hook_attn_out", lambda hv, hook: R.layer_addition_hook(hv, hook, vecs[1]))])[0, -1]
+        _, c0 = oracle.run_with_cache(torch.tensor([p]))
+        _, c2 = oracle.run_with_cache(torch.tensor([prompts[2]]))
+        r = c0["blocks.1.hook_resid_pre"].clone()
+        r[0, 100] = c2["blocks.1.hook_resid_pre"][0, 600]
+        w2 = oracle.forward(r, start_at_layer=1)[0, -1]
+        for j, want in enumerate((w0, w1, w2)):
+            assert rel_err(got[j], want) < 1e-4, (gemm, j)
+        del model

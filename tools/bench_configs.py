@@ -68,25 +68,36 @@ def c2_c3(which, gemm):
 
 
 def c4(n_tasks, gemm):
-    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device="cuda", gemm=gemm)
+    """C4 through the multi-GPU entry points (distributed.py), which are the
+    plain functions when run as one process: extraction prompt-sharded (one
+    all-reduce of [L, d]), CIE head-sharded (one all-reduce of [L, H]), the FV
+    layer sweep with (prompt, layer) sites round-robin (one all_gather).
+    torchrun: every rank builds the same seeded prompts and gets the same
+    results; rank 0 reports."""
+    from tvr_amd import distributed as D
+    rank, world = D.world()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device=dev, gemm=gemm)
     arrow = tvr_amd.tasks.ARROW
     per_task = []
     for ti in range(n_tasks):
         task = tvr_amd.tasks.synthetic_task(50, model.cfg.d_vocab, seed=100 + ti)
         random.seed(ti)
         t0 = time.perf_counter()
-        mean, t_ex = timed(lambda: E.generate_mean_activation(task, arrow, ",", model=model, num_contexts=512,
-                                                              len_contexts=5))
+        ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, task, arrow, ",", 512, 5)
+        mean, t_ex = timed(lambda: D.mean_activation_sharded(ex_prompts, model))
         prompts, answers = E.generate_shuffled_prompts(task, model, 12, 5, arrow)
-        cie, t_cie = timed(lambda: E.calculate_average_causal_indirect_effect(mean, prompts, answers, model))
+        cie, t_cie = timed(lambda: D.cie_heads_sharded(mean, prompts, answers, model))
         fv = E.assemble_task_vector(mean, cie, 10, 10)
-        acc, t_fv = timed(lambda: E.check_accuracy_of_added_task_vector_by_layer(fv, task, 5, model))
+        acc, t_fv = timed(lambda: D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, task, 5, model))
         per_task.append({"task_seed": 100 + ti, "extraction_s": round(t_ex, 3), "cie_s": round(t_cie, 3),
                          "cie_patched_prompts_per_s": round(12 * 1024 / t_cie, 1), "fv_layer_sweep_s": round(t_fv, 3),
                          "total_s": round(time.perf_counter() - t0, 3), "fv_top5_acc_by_layer": acc})
     cie_rate = sum(12 * 1024 / t["cie_s"] for t in per_task) / len(per_task)
-    return {"C4": {"gemm": gemm, "tasks": per_task, "mean_cie_patched_prompts_per_s": round(cie_rate, 1),
-                   "mean_task_s": round(sum(t["total_s"] for t in per_task) / len(per_task), 3)}}
+    return {"C4": {"gemm": gemm, "world": world, "tasks": per_task, "mean_cie_patched_prompts_per_s": round(cie_rate, 1),
+                   "mean_task_s": round(sum(t["total_s"] for t in per_task) / len(per_task), 3),
+                   "sharding": "extraction prompt-sharded + all-reduce; CIE heads = rank mod world + all-reduce; FV "
+                               "layer sweep sites round-robin + all_gather"}}
 
 
 def main():
@@ -95,7 +106,15 @@ def main():
     ap.add_argument("--gemm", default="x2f16", help="GEMM path of C2/C3 (fp32-accurate by default)")
     ap.add_argument("--c4-gemm", default="bf16", help="GEMM path of C4 (BASELINE.json: bf16)")
     ap.add_argument("--c4-tasks", type=int, default=20)
+    ap.add_argument("--dist-backend", default="nccl", help="torchrun runs: nccl (RCCL) or gloo")
     a = ap.parse_args()
+    import os
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world > 1:  # torchrun: one rank per GPU, RCCL (C4 only)
+        local = int(os.environ.get("LOCAL_RANK", 0))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(a.dist_backend)
     which = set(a.configs.split(","))
     out = {"gpu": torch.cuda.get_device_name(0), "weights": "seeded synthetic (no checkpoints offline)",
            "gemm": a.gemm}
@@ -104,7 +123,10 @@ def main():
         torch.cuda.empty_cache()
     if "C4" in which:
         out.update(c4(a.c4_tasks, a.c4_gemm))
-    print(json.dumps(out))
+    if world == 1 or dist.get_rank() == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
