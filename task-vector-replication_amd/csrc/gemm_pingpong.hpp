@@ -23,14 +23,17 @@
 //
 // Staging (LDS-DMA, 2 buffers): a k-tile is 4 regions of 16 KB (A_lo = rows
 // 0-63 of each wave-row's 128, A_hi, W_lo = columns 0-31 of each wave-column's
-// 64, W_hi), each 16 x 1 KB pieces, 2 per wave.  A region is restaged for the
-// tile two ahead (same buffer) two phases after its last read — q1 stages
-// A_hi(t+1), q3 A_lo(t+2) and W_lo(t+2), q4 W_hi(t+2) — which is the WAR
-// margin the one-barrier group offset needs (a wave of the other group may
-// still be reading one segment later).  Every region lands >= 6 phases after it
-// is issued and is retired one phase before its first read by a COUNTED wait:
-// vmcnt(8) before the stage of q1, q2 and q4 (8 = the glds issued since), then
-// the phase's barrier; nothing in the loop waits vmcnt(0) and no
+// 64, W_hi), each 16 x 1 KB pieces, 2 per wave.  Exactly one region is staged
+// per phase — q1 A_hi(t+1), q2 W_hi(t+1), q3 A_lo(t+2), q4 W_lo(t+2) — so no
+// read segment carries more than 2 glds (their issue cost, not LDS bandwidth,
+// is what makes a read segment outlast its partner's 24-MFMA cluster; 4 glds in
+// one segment cost 1-3 % of the loop, tools/gemm_split_probe x2pp9 in r02).
+// Each region is restaged >= 2 phases after its last read (the WAR margin the
+// one-barrier group offset needs: a wave of the other group may still be
+// reading one segment later), lands >= 3 phases after it is issued, and is
+// retired one phase before its first read by a COUNTED wait (the glds issued
+// since): vmcnt(4) in q1 (W_hi), vmcnt(8) in q2 (A_hi), vmcnt(6) in q4 (A_lo,
+// W_lo), then the phase's barrier; nothing in the loop waits vmcnt(0) and no
 // __syncthreads() (its fence would drain the DMA).  Past the last k-tile the
 // stage still issues (same counts) into a 1 KB LDS region nobody reads.
 #pragma once
@@ -194,8 +197,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
 // (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
-// waits in the loop (racy: timing only), 5 LDS-DMA issued inside the MFMA
-// clusters instead of the read segments, 6 per-block stamps (start, loop
+// waits in the loop (racy: timing only), 6 per-block stamps (start, loop
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only).
@@ -332,21 +334,16 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   __builtin_amdgcn_sched_barrier(0);         \
   __builtin_amdgcn_s_barrier();              \
   __builtin_amdgcn_sched_barrier(0)
-  // an MFMA cluster with LDS-DMA issues pinned between its parts
-#define TVR_PP_PIN(...)              \
-  __builtin_amdgcn_sched_barrier(0); \
-  __VA_ARGS__;                       \
-  __builtin_amdgcn_sched_barrier(0)
 
-  // ---- prologue: the stage history of tiles -2 and -1, then retire A_lo(0) / W_lo(0)
+  // ---- prologue: the stage history of tiles -2 and -1 in loop order (A_lo W_lo
+  // A_hi W_hi of tile 0, A_lo W_lo of tile 1), then retire A_lo(0) / W_lo(0)
   stage(0, 0);
   stage(2, 0);
-  stage(3, 0);
   stage(1, 0);
+  stage(3, 0);
   stage(0, 1);
   stage(2, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  stage(3, 1);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   if (wr == 1 && VAR != 3) {  // the group offset: waves 4-7 run one barrier behind
@@ -358,43 +355,27 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
   for (int kt = 0; kt < nk; ++kt) {
     const uint16_t* cur = lds + (kt & 1) * BUF;
-    if constexpr (VAR == 5) {  // LDS-DMA issued inside the MFMA clusters (same order, same counts)
-      read_a(cur, 0);
-      read_w(cur, 0, fwl);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, 0, 2); TVR_PP_PIN(stage(1, kt + 1)); mfma_quadrant(0, 0, fwl, 2, 4));
-      read_w(cur, 2, fwh);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh));
-      read_a(cur, 4);
-      TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, 0, 1); TVR_PP_PIN(stage(0, kt + 2)); mfma_quadrant(4, 2, fwh, 1, 2);
-                     TVR_PP_PIN(stage(2, kt + 2)); mfma_quadrant(4, 2, fwh, 2, 4));
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, 0, 2); TVR_PP_PIN(stage(3, kt + 2)); mfma_quadrant(4, 0, fwl, 2, 4));
-      continue;
-    }
     // q1: Q(A_lo, W_lo)
     read_a(cur, 0);
     read_w(cur, 0, fwl);
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // W_hi(kt), read in q2
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
     stage(1, kt + 1);
     TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl));
     // q2: Q(A_lo, W_hi)
     read_w(cur, 2, fwh);
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt), read in q3
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+    stage(3, kt + 1);
     TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh));
     // q3: Q(A_hi, W_hi)
     read_a(cur, 4);
     stage(0, kt + 2);
-    stage(2, kt + 2);
     TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh));
     // q4: Q(A_hi, W_lo)
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1), read in q1
-    stage(3, kt + 2);
+    if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
+    stage(2, kt + 2);
     TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl));
   }
 #undef TVR_PP_CLUSTER
-#undef TVR_PP_PIN
   if constexpr (VAR == 6 || VAR == 8) d_loop1 = __builtin_amdgcn_s_memtime();
   if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sink's DMAs retire before the block ends
