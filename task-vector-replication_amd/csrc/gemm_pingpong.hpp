@@ -200,7 +200,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
 // waits in the loop (racy: timing only), 6 per-block stamps (start, loop
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
-// skipped (timing only).
+// skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
+// same instruction stream: timing only).
 template <int EPI, int FMT, bool VEC = true, int VAR = 0>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
@@ -271,7 +272,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   auto stage = [&](int R, int kt) {
     if (VAR == 1 && kt >= 2) return;
     const bool live = kt < nk;
-    const int koff = live ? (kbeg + kt) * BK : 0;
+    const int koff = live && VAR != 12 ? (kbeg + kt) * BK : 0;  // VAR 12: every k-tile re-reads k-tile 0 (L2-hot)
     const int boff = (kt & 1) * BUF;
 #pragma unroll
     for (int s = 0; s < 2; ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));

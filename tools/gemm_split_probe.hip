@@ -140,11 +140,12 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4") {  // diagnostic variants
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12") {  // diagnostic variants
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
                     : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
                     : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
+                    : path == "x2pp12" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 12>
                                       : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
           hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
