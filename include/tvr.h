@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 6
+#define TVR_ABI_VERSION 7
 
 enum tvr_status {
   TVR_OK = 0,
@@ -181,6 +181,21 @@ int tvr_forward_clean(tvr_model* model, tvr_trace* trace, const int32_t* tokens,
                       int32_t* out_topk, int32_t topk, float* out_logits,
                       float* capture_zsum, void* stream);
 
+/* tvr_forward_clean (no logits, no capture) deferred into the next
+ * tvr_patch_sweep on `trace`: that sweep runs the clean rows in its own
+ * launches (one staircase instead of a clean forward + a staircase), fills the
+ * trace exactly as tvr_forward_clean would, and writes out_prob / out_topk
+ * (stream-ordered: read them after that sweep).  Any other use of the trace
+ * first (tvr_trace_read, tvr_forward_clean, another deferral) runs the clean
+ * forward on its own.  Same checks and errors as tvr_forward_clean; no GPU
+ * work is enqueued by this call.  The reference's pattern it serves: a clean
+ * forward and the patched forwards of the same prompts (scratch2.py:143-148,
+ * 183-192). */
+int tvr_forward_clean_deferred(tvr_model* model, tvr_trace* trace, const int32_t* tokens,
+                               const int32_t* seq_lens, int32_t n_seq,
+                               const int32_t* targets, float* out_prob,
+                               int32_t* out_topk, int32_t topk, void* stream);
+
 /* Logits of EVERY position, out_logits device [sum(seq_lens)][V]: the
  * TransformerLens forward's [1, T, V] (scratch2.py:143,183,297;
  * scratch.py:127,143).  Exactly one input:
@@ -201,7 +216,7 @@ int tvr_forward_logits(tvr_model* model, const int32_t* tokens, const float* res
  *   vectors  device [n_vectors][d]
  *   out_prob device [n_sites], out_topk device [n_sites][topk],
  *   out_logits device [n_sites][V] or NULL                                  */
-int tvr_patch_sweep(tvr_model* model, const tvr_trace* trace,
+int tvr_patch_sweep(tvr_model* model, tvr_trace* trace,
                     const tvr_site* sites, int32_t n_sites,
                     const float* vectors, int32_t n_vectors, float* out_prob,
                     int32_t* out_topk, int32_t topk, float* out_logits,

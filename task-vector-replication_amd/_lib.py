@@ -66,7 +66,7 @@ class CHbmStats(ctypes.Structure):
 HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 6  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 7  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
@@ -87,6 +87,8 @@ SIGNATURES = {
     "tvr_forward_clean": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_i32p, c_i32p, ctypes.c_int32,
                                          c_i32p, c_f32p, c_i32p, ctypes.c_int32, c_f32p, c_f32p,
                                          ctypes.c_void_p]),
+    "tvr_forward_clean_deferred": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_i32p, c_i32p, ctypes.c_int32,
+                                                  c_i32p, c_f32p, c_i32p, ctypes.c_int32, ctypes.c_void_p]),
     "tvr_forward_logits": (ctypes.c_int, [ctypes.c_void_p, c_i32p, c_f32p, ctypes.c_int32, c_i32p, ctypes.c_int32,
                                           c_f32p, ctypes.c_void_p]),
     "tvr_patch_sweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,

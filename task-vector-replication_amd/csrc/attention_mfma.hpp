@@ -42,12 +42,14 @@ constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 // MFMA chains, global loads): as many waves per SIMD as the fragments allow
 // without spilling (4 at one key tile, 3 up to four, else 2).
 // zf_last: the fp32 hook_z copy only for each sequence's last row, at row s of
-// zf (the extraction's capture reads nothing else), instead of every row.
+// zf (the extraction's capture reads nothing else), instead of every row;
+// otherwise rows below zf_rows only (a fused clean + patch sweep traces its
+// clean rows, which come first).
 template <int FMT, int DH, int NKT>
 __global__ void __launch_bounds__(64 * ATTM_WAVES, (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
 attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
                       const SeqDesc* __restrict__ seqs, int n_seqs, int n_heads, void* __restrict__ z, int ldz,
-                      float* __restrict__ zf, int ldzf, int zf_last, unsigned* __restrict__ flag,
+                      float* __restrict__ zf, int ldzf, int zf_last, int zf_rows, unsigned* __restrict__ flag,
                       const float* __restrict__ cos_t, const float* __restrict__ sin_t, int d,
                       float inv_attn_scale) {
   typedef float f4 __attribute__((ext_vector_type(4)));
@@ -275,7 +277,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
           store_act4<FMT>((uint16_t*)z + zrow * 2 * ldz + col, ldz, v[0], v[1], v[2], v[3], flag);
         else
           *(f4*)((float*)z + zrow * ldz + col) = v;
-        if (zf && !zf_last) *(f4*)(zf + zrow * ldzf + col) = v;
+        if (zf && !zf_last && zrow < (size_t)zf_rows) *(f4*)(zf + zrow * ldzf + col) = v;
         if (zf && zf_last && q0 + li == sd.n - 1) *(f4*)(zf + (size_t)s * ldzf + col) = v;
       }
     }

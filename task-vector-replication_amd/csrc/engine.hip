@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -133,6 +134,16 @@ struct tvr_trace {
   std::vector<int> seq_off, seq_len;
   std::vector<int32_t> tokens;  // host copy of the traced ids (shared-prefix detection in patch sweeps)
   int n_seq = 0, n_tokens = 0;
+  // A deferred clean forward (tvr_forward_clean_deferred): the metadata above
+  // is set, the buffers are not; the next tvr_patch_sweep on this trace runs
+  // the clean rows inside its own launches (filling the buffers as
+  // tvr_forward_clean would) and writes these outputs; any other use of the
+  // trace runs it on its own first (flush_pending).
+  bool pending = false;
+  std::vector<int32_t> p_targets;  // [n_seq] or empty
+  float* p_prob = nullptr;
+  int32_t* p_topk = nullptr;
+  int p_k = 0;
 };
 
 namespace {
@@ -515,7 +526,8 @@ struct Acts {
 // the Pythia head sizes d_head 16 (tiny), 64, 80, 128 with rotary_dim =
 // d_head / 4 (every Pythia: rotary_pct 0.25); check_config rejects the rest.
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
-                     int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st, bool zf_last = false) {
+                     int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st, bool zf_last = false,
+                     int zf_rows = INT_MAX) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
@@ -527,7 +539,7 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 0;
 #define TVR_ATTM(F, DHV, NK)                                                                                        \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
-                     n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, m->range_flag, m->rot_cos, m->rot_sin, d, \
+                     n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
                      inv_scale)
 #define TVR_ATTM_NK(F, DHV)                                                                     \
   if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                            \
@@ -588,7 +600,8 @@ double attention_bytes(int d, int q_rows, int kv_rows, int fmt, int zf_rows) {
 
 // zf_last: the fp32 hook_z copy of each sequence's last row only, at row s of zf
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
-              Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st, bool zf_last = false) {
+              Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st, bool zf_last = false,
+              int zf_rows = INT_MAX) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -597,8 +610,8 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, R, m->D1, d,
                       e1, st, m));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last));
-  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf ? (zf_last ? n_seqs : R) : 0));
+  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf ? (zf_last ? n_seqs : std::min(R, zf_rows)) : 0));
   return TVR_OK;
 }
 
@@ -610,7 +623,7 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
 // (nothing downstream reads the final residual).
 int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT, Acts& a,
                         const float* cache_qkv, const int32_t* d_last, int n_last, bool write_out,
-                        float* zf, hipStream_t st, bool zf_last = false) {
+                        float* zf, hipStream_t st, bool zf_last = false, int zf_rows = INT_MAX) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -628,8 +641,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, n_last, m->D1,
                       d, e1, st, m));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last));
-  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? n_last : 0));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
+  ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? std::min(n_last, zf_rows) : 0));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
   e2.bias = w.b2;
@@ -734,6 +747,10 @@ int check_config(const tvr_config& c) {
 }  // namespace
 
 // ===========================================================================
+namespace {
+int flush_pending(tvr_trace* t, void* stream);
+}  // namespace
+
 extern "C" {
 
 const char* tvr_version(void) {
@@ -996,6 +1013,7 @@ int tvr_trace_destroy(tvr_trace* t) {
 
 int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, void* stream) {
   if (!t || !dst) return fail(TVR_ERR_INVALID, "tvr_trace_read: null argument");
+  TVR_TRY(flush_pending(const_cast<tvr_trace*>(t), stream));  // a deferred clean forward runs now
   const int L = t->model->cfg.n_layers, d = t->model->cfg.d_model;
   const size_t stride = (size_t)t->max_tokens * d;
   const float* src = nullptr;
@@ -1186,6 +1204,15 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
                       (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st));
   return TVR_OK;
 }
+// Run a deferred clean forward on its own (the trace is used other than by a
+// patch sweep).
+int flush_pending(tvr_trace* t, void* stream) {
+  if (!t->pending) return TVR_OK;
+  t->pending = false;
+  const std::vector<int32_t> tok(t->tokens), lens(t->seq_len), tg(t->p_targets);
+  return forward_impl(t->model, t, tok.data(), nullptr, 0, lens.data(), (int32_t)lens.size(),
+                      tg.empty() ? nullptr : tg.data(), t->p_prob, t->p_topk, t->p_k, nullptr, false, nullptr, stream);
+}
 }  // namespace
 
 extern "C" {
@@ -1194,8 +1221,47 @@ int tvr_forward_clean(tvr_model* m, tvr_trace* trace, const int32_t* tokens, con
                       int32_t n_seq, const int32_t* targets, float* out_prob, int32_t* out_topk,
                       int32_t topk, float* out_logits, float* capture_zsum, void* stream) {
   if (!tokens) return fail(TVR_ERR_INVALID, "tvr_forward_clean: bad argument");
+  if (trace) TVR_TRY(flush_pending(trace, stream));  // its outputs are owed to the caller
   return forward_impl(m, trace, tokens, nullptr, 0, seq_lens, n_seq, targets, out_prob, out_topk, topk, out_logits,
                       false, capture_zsum, stream);
+}
+
+int tvr_forward_clean_deferred(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const int32_t* seq_lens,
+                               int32_t n_seq, const int32_t* targets, float* out_prob, int32_t* out_topk,
+                               int32_t topk, void* stream) {
+  if (!m || !trace || !tokens || !seq_lens || n_seq <= 0)
+    return fail(TVR_ERR_INVALID, "tvr_forward_clean_deferred: bad argument");
+  if (trace->model != m) return fail(TVR_ERR_INVALID, "trace belongs to another model");
+  if (topk < 0 || topk > STATS_MAX_K) return fail(TVR_ERR_INVALID, "topk must be in [0, 16]");
+  if (topk > 0 && !out_topk) return fail(TVR_ERR_INVALID, "topk > 0 needs out_topk");
+  TVR_TRY(flush_pending(trace, stream));
+  const tvr_config& c = m->cfg;
+  std::vector<int> off(n_seq);
+  int R = 0;
+  for (int s = 0; s < n_seq; ++s) {
+    const int T = seq_lens[s];
+    if (T <= 0) return fail(TVR_ERR_INVALID, "sequence " + std::to_string(s) + " is empty");
+    if (T > c.n_ctx)
+      return fail(TVR_ERR_UNSUPPORTED, "sequence length " + std::to_string(T) + " exceeds n_ctx " +
+                                           std::to_string(c.n_ctx));
+    off[s] = R;
+    R += T;
+  }
+  for (int r = 0; r < R; ++r)
+    if (tokens[r] < 0 || tokens[r] >= c.d_vocab)
+      return fail(TVR_ERR_INVALID, "token id " + std::to_string(tokens[r]) + " out of range");
+  if (n_seq > trace->max_seqs || R > trace->max_tokens) return fail(TVR_ERR_INVALID, "trace capacity exceeded");
+  trace->seq_off = off;
+  trace->seq_len.assign(seq_lens, seq_lens + n_seq);
+  trace->tokens.assign(tokens, tokens + R);
+  trace->n_seq = n_seq;
+  trace->n_tokens = R;
+  trace->p_targets = targets ? std::vector<int32_t>(targets, targets + n_seq) : std::vector<int32_t>();
+  trace->p_prob = out_prob;
+  trace->p_topk = out_topk;
+  trace->p_k = topk;
+  trace->pending = true;
+  return TVR_OK;
 }
 
 int tvr_forward_logits(tvr_model* m, const int32_t* tokens, const float* resid_in, int32_t start_layer,
@@ -1208,7 +1274,7 @@ int tvr_forward_logits(tvr_model* m, const int32_t* tokens, const float* resid_i
 
 
 
-int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites, int32_t n_sites,
+int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32_t n_sites,
                     const float* vectors, int32_t n_vectors, float* out_prob, int32_t* out_topk,
                     int32_t topk, float* out_logits, void* stream) {
   if (!m || !trace || !sites || n_sites <= 0)
@@ -1220,10 +1286,18 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   hipStream_t st = (hipStream_t)stream;
   const tvr_config& c = m->cfg;
   const int d = c.d_model, L = c.n_layers;
+  // Fused clean forward (a deferred tvr_forward_clean on this trace): the
+  // clean rows [0, Rc) (trace row layout) run in the same launches as the
+  // site rows, which follow them; the sites read the clean K/V from the live
+  // buffer, and the trace is filled as the layers go.  This removes the clean
+  // forward's own small-M launches (52 prompts x 3 tokens).
+  const bool fused = trace->pending;
+  const int Rc = fused ? trace->n_tokens : 0, nc = fused ? trace->n_seq : 0;
 
   // --- plan -----------------------------------------------------------------
   std::vector<int> entry(n_sites), p0(n_sites), nrow(n_sites);
   int maxT = 0;
+  for (int s = 0; s < nc; ++s) maxT = std::max(maxT, trace->seq_len[s]);
   for (int i = 0; i < n_sites; ++i) {
     const tvr_site& s = sites[i];
     if (s.seq < 0 || s.seq >= trace->n_seq)
@@ -1312,17 +1386,19 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
       rows_le[l] = rows;
     }
   }
-  std::vector<SeqDesc> seqs(n_sites);
+  // sequence descriptors: the fused clean sequences first, then the sites in entry order
+  std::vector<SeqDesc> seqs(nc + n_sites);
+  for (int s = 0; s < nc; ++s) seqs[s] = SeqDesc{trace->seq_off[s], trace->seq_len[s], 0, -1, 0, 0};
   std::vector<EntryDesc> ents(n_sites);
   for (int k = 0; k < n_sites; ++k) {
     const int i = order[k];
     const tvr_site& s = sites[i];
     const int srow = trace->seq_off[s.seq];
-    seqs[k] = leader[i] >= 0 ? SeqDesc{row0[i], nrow[i], p0[i], row0[leader[i]], 0, 1}
-                             : SeqDesc{row0[i], nrow[i], p0[i], srow, 0, 0};
+    seqs[nc + k] = leader[i] >= 0 ? SeqDesc{Rc + row0[i], nrow[i], p0[i], Rc + row0[leader[i]], 0, 1}
+                                  : SeqDesc{Rc + row0[i], nrow[i], p0[i], srow, 0, 0};
     EntryDesc e{};
     e.kind = s.kind;
-    e.row0 = row0[i];
+    e.row0 = Rc + row0[i];
     e.n = nrow[i];
     e.p0 = p0[i];
     e.src_row = srow;
@@ -1349,31 +1425,42 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
       entry_bytes[l] += b;
     }
   }
-  std::vector<int32_t> last(n_sites), tg(n_sites), last_sorted(n_sites);
+  std::vector<int32_t> last(n_sites), tg(n_sites);
   for (int i = 0; i < n_sites; ++i) {
-    last[i] = row0[i] + nrow[i] - 1;
+    last[i] = Rc + row0[i] + nrow[i] - 1;
     tg[i] = sites[i].target;
   }
+  // the last layer computes every clean row (the trace keeps them) and each site's last row
   std::vector<SeqDesc> seqs_last(seqs);
+  std::vector<int32_t> last_sorted(Rc + n_sites);
+  for (int r = 0; r < Rc; ++r) last_sorted[r] = r;
   for (int k = 0; k < n_sites; ++k) {
-    seqs_last[k].q0 = seqs_last[k].n - 1;
-    last_sorted[k] = last[order[k]];
+    seqs_last[nc + k].q0 = seqs_last[nc + k].n - 1;
+    last_sorted[Rc + k] = last[order[k]];
   }
+  std::vector<int32_t> clean_last(nc), clean_tg(nc, -1);
+  for (int s = 0; s < nc; ++s) clean_last[s] = trace->seq_off[s] + trace->seq_len[s] - 1;
+  if (fused && !trace->p_targets.empty()) clean_tg = trace->p_targets;
+  const int ktop = std::max(topk, fused ? trace->p_k : 0);
 
-  const int FC = std::min(kFinalChunk, n_sites);
+  const int RA = Rc + R;  // rows of the activation buffers
+  const int FC = std::min(kFinalChunk, std::max(n_sites, nc));
   Carve cv;
-  const size_t o_seqs = cv.take<SeqDesc>(n_sites);
-  const size_t o_seqs_last = cv.take<SeqDesc>(n_sites);
-  const size_t o_last_sorted = cv.take<int32_t>(n_sites);
+  const size_t o_seqs = cv.take<SeqDesc>(nc + n_sites);
+  const size_t o_seqs_last = cv.take<SeqDesc>(nc + n_sites);
+  const size_t o_last_sorted = cv.take<int32_t>(Rc + n_sites);
   const size_t o_ents = cv.take<EntryDesc>(n_sites);
   const size_t o_last = cv.take<int32_t>(n_sites);
   const size_t o_tg = cv.take<int32_t>(n_sites);
-  const size_t o_resid = cv.take<float>((size_t)R * d);
-  const size_t o_xn = cv.take<float>((size_t)R * d);
-  const size_t o_qkv = cv.take<float>((size_t)R * 3 * d);
-  const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
+  const size_t o_clast = cv.take<int32_t>(nc);
+  const size_t o_ctg = cv.take<int32_t>(nc);
+  const size_t o_ctok = cv.take<int32_t>(Rc);
+  const size_t o_resid = cv.take<float>((size_t)RA * d);
+  const size_t o_xn = cv.take<float>((size_t)RA * d);
+  const size_t o_qkv = cv.take<float>((size_t)RA * 3 * d);
+  const size_t o_a2 = cv.take<float>((size_t)RA * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
-  const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, topk, out_logits));
+  const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, ktop, out_logits));
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -1383,6 +1470,11 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   ub.add(o_ents, ents);
   ub.add(o_last, last);
   ub.add(o_tg, tg);
+  if (fused) {
+    ub.add(o_clast, clean_last);
+    ub.add(o_ctg, clean_tg);
+    ub.add(o_ctok, std::vector<int32_t>(trace->tokens.begin(), trace->tokens.begin() + Rc));
+  }
   TVR_TRY(flush_uploads(m, st, base, ub));
 
   const int fmt = act_fmt(m);
@@ -1391,6 +1483,13 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const EntryDesc* d_ents = (const EntryDesc*)(base + o_ents);
   const size_t tstride = (size_t)trace->max_tokens * d;
+  const size_t rbytes = (size_t)Rc * d * sizeof(float);  // the clean rows of one [rows][d] buffer
+  if (fused) {
+    const size_t total = (size_t)Rc * (d / 4);
+    hipLaunchKernelGGL(embed_kernel, dim3((int)std::min<size_t>((total + 255) / 256, 8192)), dim3(256), 0, st,
+                       (const int32_t*)(base + o_ctok), m->w_embed, a.resid, Rc, d);
+    TVR_HIP(hipGetLastError());
+  }
 
   auto enter = [&](int l) -> int {
     const int k0 = l > 0 ? cnt_le[l - 1] : 0, k1 = cnt_le[l];
@@ -1412,21 +1511,36 @@ int tvr_patch_sweep(tvr_model* m, const tvr_trace* trace, const tvr_site* sites,
   };
 
   for (int l = 0; l < L; ++l) {
+    if (fused)  // hook_resid_pre of the clean rows (the entries below read it from the trace)
+      TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, rbytes, hipMemcpyDeviceToDevice, st));
     TVR_TRY(enter(l));
-    const int Rl = rows_le[l];
+    const int Rl = Rc + rows_le[l];
     if (Rl == 0) continue;
-    const float* cache = trace->qkv + (size_t)l * 3 * tstride;
+    float* tqkv = trace->qkv + (size_t)l * 3 * tstride;
+    const float* cache = fused ? a.qkv : tqkv;
+    float* zf = fused ? trace->z + l * tstride : nullptr;  // the clean rows' hook_z (rows < Rc)
     if (l == L - 1) {
-      TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), cnt_le[l], maxT, a, cache,
-                                  (const int32_t*)(base + o_last_sorted), cnt_le[l], true, nullptr, st));
+      TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), nc + cnt_le[l], maxT, a, cache,
+                                  (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc));
     } else {
-      TVR_TRY(run_block(m, l, Rl, d_seqs, cnt_le[l], maxT, a, a.qkv, cache, nullptr, st));
+      TVR_TRY(run_block(m, l, Rl, d_seqs, nc + cnt_le[l], maxT, a, a.qkv, cache, zf, st, false, Rc));
       TVR_TRY(run_block_out(m, l, Rl, a, st));
     }
+    if (fused)
+      TVR_HIP(hipMemcpyAsync(tqkv, a.qkv, 3 * rbytes, hipMemcpyDeviceToDevice, st));
+  }
+  if (fused) {
+    TVR_HIP(hipMemcpyAsync(trace->resid + L * tstride, a.resid, rbytes, hipMemcpyDeviceToDevice, st));
+    trace->pending = false;
   }
   TVR_TRY(enter(L));
-  return run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
-                   (float*)(base + o_xf), (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st);
+  TVR_TRY(run_final(m, a.resid, (const int32_t*)(base + o_last), (const int32_t*)(base + o_tg), n_sites,
+                    (float*)(base + o_xf), (float*)(base + o_lg), out_prob, out_topk, topk, out_logits, fmt, st));
+  if (fused && (trace->p_prob || trace->p_topk))
+    TVR_TRY(run_final(m, a.resid, (const int32_t*)(base + o_clast), (const int32_t*)(base + o_ctg), nc,
+                      (float*)(base + o_xf), (float*)(base + o_lg), trace->p_prob, trace->p_topk, trace->p_k,
+                      nullptr, fmt, st));
+  return TVR_OK;
 }
 
 int tvr_project_heads(tvr_model* m, const float* zsum, float* out, void* stream) {

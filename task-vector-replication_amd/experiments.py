@@ -103,7 +103,8 @@ def _add_site_outputs(model: Model, seqs: List[List[int]], site_seq, site_layer,
     n_sites = len(site_seq)
     sel = np.arange(n_sites) if shard is None else np.asarray(shard.select(n_sites), dtype=np.int64)
     trace = model._sweep_trace(len(seqs), sum(len(s) for s in seqs))
-    clean = model.forward_clean(seqs, targets=targets, topk=topk, trace=trace)
+    # the clean rows run inside the first sweep launch when there is one
+    clean = model.forward_clean(seqs, targets=targets, topk=topk, trace=trace, defer=len(sel) > 0)
     dev = model.device
     patched = {}
     if targets is not None:
@@ -217,7 +218,7 @@ def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Se
         tg = [int(t) for t in answers[a:b]]
         n = len(seqs)
         trace = model._sweep_trace(n, sum(len(s) for s in seqs))
-        p0 = model.forward_clean(seqs, targets=tg, trace=trace)["prob"]
+        p0 = model.forward_clean(seqs, targets=tg, trace=trace, defer=per_prompt > 0)["prob"]
         sites = make_sites(n * per_prompt)
         sites["seq"] = np.repeat(np.arange(n, dtype=np.int32), per_prompt)
         sites["kind"] = _lib.SITE_REPLACE_HEAD_ALLPOS

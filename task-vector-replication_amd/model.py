@@ -51,6 +51,9 @@ class Trace:
         self.max_tokens = max_tokens
         self.seq_lens: List[int] = []
         self.seq_offsets: List[int] = []
+        # output tensors of a deferred clean forward, kept alive until the
+        # engine has written them (the next patch sweep or trace read)
+        self._pending_out = None
 
     def resid_pre(self, layer: int) -> torch.Tensor:
         """``blocks.{layer}.hook_resid_pre`` of every traced token ([tokens, d]);
@@ -66,6 +69,7 @@ class Trace:
         buf = torch.empty(sum(self.seq_lens), m.cfg.d_model, device=m.device)
         _lib.check(self._lib.tvr_trace_read(self._h, what, layer, buf.data_ptr(), m._stream()),
                    "tvr_trace_read")
+        self._pending_out = None
         return buf
 
     def __del__(self):
@@ -203,11 +207,14 @@ class Model(TokenizerMixin):
     # ---------------------------------------------------------- entry points
     def forward_clean(self, seqs: Sequence[Sequence[int]], targets: Optional[Sequence[int]] = None,
                       topk: int = 0, return_logits: bool = False, capture: bool = False,
-                      trace: Optional[Trace] = None) -> Dict[str, torch.Tensor]:
+                      trace: Optional[Trace] = None, defer: bool = False) -> Dict[str, torch.Tensor]:
         """Batched clean forward of ragged prompts (token-id lists).
         Returns ``prob`` [n] (softmax(logits[-1])[target]), ``topk`` [n, k],
         ``logits`` [n, V] (last position), ``zsum`` [L, d] (sum over prompts of
-        hook_z at the last position) as requested."""
+        hook_z at the last position) as requested.
+        ``defer`` (with a trace; no logits / capture): the clean rows run inside
+        the next ``patch_sweep`` on that trace (tvr_forward_clean_deferred) and
+        the returned tensors are written by it — read them after that sweep."""
         n = len(seqs)
         if n == 0:
             raise ValueError("no prompts")
@@ -225,6 +232,17 @@ class Model(TokenizerMixin):
         zsum = torch.zeros(self.cfg.n_layers, self.cfg.d_model, device=dev) if capture else None
         if trace is not None and (trace.max_seqs < n or trace.max_tokens < int(lens.sum())):
             raise ValueError("trace too small for this batch")
+        if defer:
+            if trace is None or logits is not None or zsum is not None:
+                raise ValueError("defer needs a trace and no logits / capture")
+            rc = self._lib.tvr_forward_clean_deferred(
+                self._h, trace._h, toks.ctypes.data, lens.ctypes.data, n,
+                tg.ctypes.data if tg is not None else None, _lib.ptr(prob), _lib.ptr(top), topk, self._stream())
+            _lib.check(rc, "tvr_forward_clean_deferred")
+            trace.seq_lens = lens.tolist()
+            trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
+            trace._pending_out = (prob, top)
+            return {k: v for k, v in (("prob", prob), ("topk", top)) if v is not None}
         rc = self._lib.tvr_forward_clean(
             self._h, trace._h if trace is not None else None,
             toks.ctypes.data, lens.ctypes.data, n,
@@ -233,6 +251,7 @@ class Model(TokenizerMixin):
         _lib.check(rc, "tvr_forward_clean")
         self._check_range("tvr_forward_clean")
         if trace is not None:
+            trace._pending_out = None
             trace.seq_lens = lens.tolist()
             trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
         if prob is not None:
@@ -268,6 +287,7 @@ class Model(TokenizerMixin):
                                        self._stream())
         _lib.check(rc, "tvr_patch_sweep")
         self._check_range("tvr_patch_sweep")
+        trace._pending_out = None
         out = {}
         if prob is not None:
             out["prob"] = prob

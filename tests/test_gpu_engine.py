@@ -799,3 +799,87 @@ def test_sequences_longer_than_128(tiny_cfg, tiny_sd, tokenizer):
         for j, want in enumerate((w0, w1, w2)):
             assert rel_err(got[j], want) < 1e-4, (gemm, j)
         del model
+
+
+def _all_kind_sites(cfg, prompts):
+    """Every site kind on every prompt (the kinds test's layout, no oracle)."""
+    sites = tvr_amd.make_sites(4 * len(prompts))
+    k = 0
+    for i, p in enumerate(prompts):
+        for kind in range(4):
+            s = sites[k]
+            s["seq"], s["kind"], s["target"] = i, kind, p[1]
+            if kind == 1:
+                s["layer"], s["head"], s["vec"] = (i + 1) % cfg.n_layers, i % cfg.n_heads, i % 5
+            elif kind == 2:
+                s["layer"], s["vec"] = i % cfg.n_layers, 4
+            elif kind == 3:
+                src = (i + 1) % len(prompts)
+                s["layer"], s["pos"], s["src_seq"], s["src_pos"] = i % cfg.n_layers, len(p) // 2, src, \
+                    len(prompts[src]) // 3
+            k += 1
+    return sites
+
+
+def test_deferred_clean_forward_fused_into_sweep(tiny_model):
+    """tvr_forward_clean_deferred + tvr_patch_sweep (the clean rows run inside
+    the sweep's launches) gives the outputs of tvr_forward_clean +
+    tvr_patch_sweep: every site kind, shared-prefix prompts, clean prob /
+    top-k, and a trace filled as the clean forward fills it (resid_pre, z,
+    and a second sweep that reads its K/V)."""
+    cfg = tiny_model.cfg
+    rng = random.Random(23)
+    base = [0] + [rng.randrange(1, cfg.d_vocab) for _ in range(29)]
+    prompts = ragged_prompts(4, cfg.d_vocab, 12, lo=3, hi=30) + [base[:24], base[:20] + [7, 9, 11], base[:24]]
+    n, ntok = len(prompts), sum(map(len, prompts))
+    tg = [p[1] for p in prompts]
+    vecs = torch.randn(5, cfg.d_model, generator=torch.Generator().manual_seed(5)).cuda()
+    sites = _all_kind_sites(cfg, prompts)
+    head = tvr_amd.make_sites(2 * n)  # head replacement on every prompt (prefix sharing between 4..6)
+    for i in range(n):
+        for j in range(2):
+            s = head[2 * i + j]
+            s["seq"], s["kind"], s["target"] = i, tvr_amd._lib.SITE_REPLACE_HEAD_ALLPOS, tg[i]
+            s["layer"], s["head"], s["vec"] = j, (i + j) % cfg.n_heads, j
+    sites = np.concatenate([sites, head])
+
+    ref_trace = tiny_model.trace(n, ntok)
+    ref_clean = tiny_model.forward_clean(prompts, targets=tg, topk=3, trace=ref_trace)
+    ref = tiny_model.patch_sweep(ref_trace, sites, vecs, topk=3, return_logits=True)
+
+    trace = tiny_model.trace(n, ntok)
+    clean = tiny_model.forward_clean(prompts, targets=tg, topk=3, trace=trace, defer=True)
+    out = tiny_model.patch_sweep(trace, sites, vecs, topk=3, return_logits=True)
+    assert rel_err(out["logits"], ref["logits"]) < 1e-5
+    assert torch.equal(out["topk"], ref["topk"])
+    assert (out["prob"] - ref["prob"]).abs().max().item() <= 1e-6
+    assert (clean["prob"] - ref_clean["prob"]).abs().max().item() <= 1e-6
+    assert torch.equal(clean["topk"], ref_clean["topk"])
+    for layer in (0, 1, cfg.n_layers):
+        assert rel_err(trace.resid_pre(layer), ref_trace.resid_pre(layer)) < 1e-5, layer
+    for layer in range(cfg.n_layers):
+        assert rel_err(trace.z(layer), ref_trace.z(layer)) < 1e-5, layer
+    again = tiny_model.patch_sweep(trace, sites, vecs, topk=3, return_logits=True)  # the filled trace, reused
+    assert rel_err(again["logits"], ref["logits"]) < 1e-5
+
+
+def test_deferred_clean_forward_runs_on_other_use(tiny_model):
+    """A deferred clean forward that no sweep picks up runs on its own when
+    the trace is read (or re-used by tvr_forward_clean): outputs written, trace
+    equal to the plain clean forward's."""
+    cfg = tiny_model.cfg
+    prompts = ragged_prompts(3, cfg.d_vocab, 31, lo=4, hi=20)
+    n, ntok = len(prompts), sum(map(len, prompts))
+    tg = [p[2] for p in prompts]
+    ref_trace = tiny_model.trace(n, ntok)
+    ref = tiny_model.forward_clean(prompts, targets=tg, topk=2, trace=ref_trace)
+    trace = tiny_model.trace(n, ntok)
+    clean = tiny_model.forward_clean(prompts, targets=tg, topk=2, trace=trace, defer=True)
+    assert rel_err(trace.resid_pre(1), ref_trace.resid_pre(1)) < 1e-5  # runs the deferred forward
+    assert (clean["prob"] - ref["prob"]).abs().max().item() <= 1e-6
+    assert torch.equal(clean["topk"], ref["topk"])
+    clean2 = tiny_model.forward_clean(prompts, targets=tg, trace=trace, defer=True)
+    tiny_model.forward_clean(prompts[:1], trace=trace)  # flushes clean2 first
+    assert (clean2["prob"] - ref["prob"]).abs().max().item() <= 1e-6
+    with pytest.raises(ValueError):
+        tiny_model.forward_clean(prompts, trace=trace, defer=True, return_logits=True)
