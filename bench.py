@@ -118,13 +118,23 @@ def pmc_summary(family, workload):
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
-def hbm_kernels(hbm, hbm_ex, steps):
+def hbm_kernels(hbm, hbm_ex, steps, workload):
     """Achieved GB/s of the HBM-bound kernels (HIP events around each launch,
     algorithmic bytes per include/tvr.h tvr_hbm_kind): injection, LayerNorm,
     attention and target-probability rows from the timed CIE region; capture
-    from the timed extraction."""
+    from the timed extraction.  ``traffic``: memory-side bytes per launch from
+    the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this command
+    (profiles/pmc_hbm_kernels.json, tools/prof_summary.py) when the workload
+    matches."""
     out = {"peak_gbps": HBM_PEAK_GBPS,
            "basis": "algorithmic bytes / summed HIP-event launch time (engine stream), per kernel kind"}
+    pm = {}
+    p = ROOT / "profiles" / "pmc_hbm_kernels.json"
+    if p.exists():
+        d = json.loads(p.read_text())
+        if d.get("workload") == workload:
+            pm = d.get("kernels", {})
+            out["traffic_source"] = f"{p.relative_to(ROOT)} ({d.get('source', '?')}; {d.get('note', '')})"
 
     def row(v, per):
         if not v["launches"]:
@@ -136,6 +146,8 @@ def hbm_kernels(hbm, hbm_ex, steps):
                 "achieved_gbps": round(g, 1), "frac": round(g / HBM_PEAK_GBPS, 4)}
     for k in ("entry", "lnpre", "attention", "row_stats"):
         out[k] = row(hbm[k], "_per_step")
+        if out[k] and k in pm:
+            out[k]["traffic"] = pm[k]["fetch_bytes_x2_per_launch"] + pm[k]["write_bytes_per_launch"]
     out["capture"] = row(hbm_ex["capture"], "") if hbm_ex else None
     return out
 
@@ -384,7 +396,7 @@ def main():
             "gemm_share_of_step": round(fam["ms"] / (el_prof * 1e3), 4),
             "variants": variants,
         },
-        "hbm_kernels": hbm_kernels(hbm, hbm_ex, psteps),
+        "hbm_kernels": hbm_kernels(hbm, hbm_ex, psteps, workload),
         "algorithmic": {
             "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(value * f_alg / 1e12, 2),

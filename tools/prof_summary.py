@@ -67,6 +67,49 @@ def gemm_variant(name):
     return None
 
 
+# the HBM-bound kernels (bench.py hbm_kernels names)
+HBM_KERNELS = {"entry_kernel": "entry", "lnpre_kernel": "lnpre", "attention_mfma_kernel": "attention",
+               "stats_merge_kernel": "row_stats", "row_stats_kernel": "row_stats", "capture_partial_kernel": "capture",
+               "capture_finish_kernel": "capture"}
+
+
+def hbm_kind(name):
+    for k, v in HBM_KERNELS.items():
+        if k in name:
+            return v
+    return None
+
+
+def hbm_kernel_traffic(f, w, bench):
+    """Memory-side bytes of the HBM-bound kernels from the same FETCH_SIZE /
+    WRITE_SIZE passes: per kind, launches and bytes per launch.  FETCH_SIZE is
+    given raw (x 1024) and doubled (the gfx950 correction, calibrated for
+    16-B-per-lane reads only: MI355X_MICROARCH.md HBM); next to bench.py's
+    algorithmic bytes per launch of the same kind."""
+    def per_kind(rows):
+        out = {}
+        for r in rows:
+            k = hbm_kind(r["Kernel_Name"])
+            if k:
+                o = out.setdefault(k, [0, 0.0])
+                o[0] += 1
+                o[1] += float(r["Counter_Value"]) * 1024
+        return out
+    fk, wk = per_kind(f), per_kind(w)
+    alg = {k: v.get("bytes_per_launch") for k, v in ((bench or {}).get("hbm_kernels") or {}).items()
+           if isinstance(v, dict)}
+    res = {}
+    for k, (n, fb) in fk.items():
+        wn, wb = wk.get(k, (n, 0.0))
+        r = {"launches": n, "fetch_bytes_raw_per_launch": round(fb / n), "fetch_bytes_x2_per_launch": round(2 * fb / n),
+             "write_bytes_per_launch": round(wb / max(wn, 1))}
+        if alg.get(k):
+            r["alg_bytes_per_launch"] = alg[k]
+            r["ratio_x2_to_alg"] = round((2 * fb / n + wb / max(wn, 1)) / alg[k], 2)
+        res[k] = r
+    return res
+
+
 def pmc(d):
     rows = []
     for r in csv.DictReader(open(one(d, "*counter_collection.csv"))):
@@ -179,6 +222,15 @@ def main():
             pm["mfma"] = mfma_util(pmc(a.mfma))
         summary["pmc_gemm"] = pm
         (out_dir / f"pmc_gemm_{fam}.json").write_text(json.dumps(pm, indent=1) + "\n")
+        hk = hbm_kernel_traffic(f, w, json.loads(Path(a.bench).read_text()) if a.bench else None)
+        if hk:
+            hk = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}",
+                  "workload": json.loads(Path(a.bench).read_text())["config"]["workload"] if a.bench else None,
+                  "note": "FETCH_SIZE doubling is calibrated for 16-B/lane reads; the attention kernel's V loads are "
+                          "4 B/lane, so its x2 figure is an upper bound",
+                  "kernels": hk}
+            summary["pmc_hbm_kernels"] = hk
+            (out_dir / "pmc_hbm_kernels.json").write_text(json.dumps(hk, indent=1) + "\n")
     (out_dir / f"rocprof_{a.tag}.json").write_text(json.dumps(summary, indent=1) + "\n")
     print(json.dumps(summary, indent=1)[:3000])
 
