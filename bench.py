@@ -118,7 +118,7 @@ def pmc_summary(family, workload):
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
-def hbm_kernels(hbm, hbm_ex, steps, workload):
+def hbm_kernels(hbm, hbm_ex, steps, workload=None):
     """Achieved GB/s of the HBM-bound kernels (HIP events around each launch,
     algorithmic bytes per include/tvr.h tvr_hbm_kind): injection, LayerNorm,
     attention and target-probability rows from the timed CIE region; capture
@@ -132,7 +132,7 @@ def hbm_kernels(hbm, hbm_ex, steps, workload):
     p = ROOT / "profiles" / "pmc_hbm_kernels.json"
     if p.exists():
         d = json.loads(p.read_text())
-        if d.get("workload") == workload:
+        if workload is not None and d.get("workload") == workload:
             pm = d.get("kernels", {})
             out["traffic_source"] = f"{p.relative_to(ROOT)} ({d.get('source', '?')}; {d.get('note', '')})"
 

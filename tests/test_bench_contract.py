@@ -37,3 +37,19 @@ def test_pmc_summary_keyed_on_family_and_workload():
     pmc, src = bench.pmc_summary("x2f16", d["workload"])
     assert pmc is not None and pmc["hbm_bytes_per_launch"] > 0 and src
     assert bench.pmc_summary("x2f16", "another workload") == (None, None)
+
+
+def test_hbm_kernels_pmc_traffic_keyed_on_workload():
+    """profiles/pmc_hbm_kernels.json (tools/prof_summary.py) attaches memory-side
+    bytes per launch to the matching workload's rows only."""
+    p = bench.ROOT / "profiles" / "pmc_hbm_kernels.json"
+    if not p.exists():
+        return
+    d = json.loads(p.read_text())
+    hbm = _kinds(2.0, 8e9, 4)
+    out = bench.hbm_kernels(hbm, None, steps=2, workload=d["workload"])
+    for k, v in d["kernels"].items():
+        if k in ("entry", "lnpre", "attention", "row_stats"):
+            assert out[k]["traffic"] == v["fetch_bytes_x2_per_launch"] + v["write_bytes_per_launch"]
+    other = bench.hbm_kernels(hbm, None, steps=2, workload="another workload")
+    assert all("traffic" not in (other[k] or {}) for k in ("entry", "lnpre", "attention", "row_stats"))
