@@ -798,6 +798,12 @@ def test_sequences_longer_than_128(tiny_cfg, tiny_sd, tokenizer):
         w2 = oracle.forward(r, start_at_layer=1)[0, -1]
         for j, want in enumerate((w0, w1, w2)):
             assert rel_err(got[j], want) < 1e-4, (gemm, j)
+        # the same sites with the clean forward deferred into the sweep (long rows in the fused launches)
+        trace2 = model.trace(len(prompts), sum(map(len, prompts)))
+        model.forward_clean(prompts, trace=trace2, defer=True)
+        fused = model.patch_sweep(trace2, sites, vecs.cuda(), return_logits=True, want_prob=False)["logits"]
+        assert rel_err(fused, got) < 1e-5, gemm
+        assert rel_err(trace2.z(1), trace.z(1)) < 1e-5 and rel_err(trace2.resid_pre(2), trace.resid_pre(2)) < 1e-5
         del model
 
 
