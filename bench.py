@@ -144,8 +144,8 @@ def hbm_kernels(hbm, hbm_ex, steps, workload=None):
                 "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
                 "bytes_per_launch": round(v["bytes"] / v["launches"]),
                 "achieved_gbps": round(g, 1), "frac": round(g / HBM_PEAK_GBPS, 4)}
-    for k in ("entry", "lnpre", "attention", "row_stats"):
-        out[k] = row(hbm[k], "_per_step")
+    for k in ("entry", "lnpre", "attention", "row_stats", "lin_entry"):
+        out[k] = row(hbm[k], "_per_step") if k in hbm else None
         if out[k] and k in pm:
             out[k]["traffic"] = pm[k]["fetch_bytes_x2_per_launch"] + pm[k]["write_bytes_per_launch"]
     out["capture"] = row(hbm_ex["capture"], "") if hbm_ex else None

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 7
+#define TVR_ABI_VERSION 8
 
 enum tvr_status {
   TVR_OK = 0,
@@ -294,12 +294,15 @@ enum tvr_hbm_kind {
   TVR_HBM_LNPRE = 2,      /* LayerNormPre rows -> GEMM input format */
   TVR_HBM_ATTENTION = 3,  /* attention: fp32 Q/K/V rows in, z out (activation format [+ fp32 hook_z]) */
   TVR_HBM_ROW_STATS = 4,  /* softmax target probability / top-k over one logit row per site */
-  TVR_HBM_KINDS = 5
+  TVR_HBM_LIN_ENTRY = 5,  /* linearised entry layer of REPLACE_HEAD sites (the vectors' W1 product G and
+                           * the K = d_head entry-row GEMM with its combine epilogue): entering rows' outputs
+                           * written + their clean rows' outputs read, z slices, W1 W_O planes once */
+  TVR_HBM_KINDS = 6
 };
 typedef struct tvr_hbm_stats {
-  int64_t launches[5];
-  double ms[5];     /* summed launch durations */
-  double bytes[5];  /* algorithmic bytes summed */
+  int64_t launches[6];
+  double ms[6];     /* summed launch durations */
+  double bytes[6];  /* algorithmic bytes summed */
 } tvr_hbm_stats;
 int tvr_profile_read_hbm(tvr_model* model, tvr_hbm_stats* out);
 

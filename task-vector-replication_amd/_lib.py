@@ -59,14 +59,14 @@ GEMM_VARIANTS = ("unembed", "qkv_mlpin", "o_mlpout")
 
 
 class CHbmStats(ctypes.Structure):
-    _fields_ = [("launches", ctypes.c_int64 * 5), ("ms", ctypes.c_double * 5), ("bytes", ctypes.c_double * 5)]
+    _fields_ = [("launches", ctypes.c_int64 * 6), ("ms", ctypes.c_double * 6), ("bytes", ctypes.c_double * 6)]
 
 
 # include/tvr.h enum tvr_hbm_kind
-HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats")
+HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats", "lin_entry")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 7  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 8  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}

@@ -29,6 +29,7 @@
 #include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
 #include "kernels.hpp"
+#include "lin_entry.hpp"
 
 using namespace tvr;
 
@@ -123,6 +124,15 @@ struct tvr_model {
   struct ProfRec { hipEvent_t a, b; int epi; double flops, bytes; };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
+  // Linearised entry layer (lin_entry.hpp), built on the first patch sweep that
+  // uses it in a planar mode and dropped on a mode change: for layers
+  // l = 1 .. L-2, Wsc = W1[l] W_O[l-1] as weight planes [NPL][H][D1][KP]
+  // (head-major, d_head zero-padded to KP) and c1[l] = row sums of W1[l].
+  int lin_mode = -1;
+  int lin_kp = 0;
+  uint16_t* lin_planes = nullptr;  // layer l at (l - 1) * NPL * H * D1 * KP halves
+  float* lin_c1 = nullptr;         // [L][D1]
+  std::vector<float> lin_scale;    // per layer: X2F16 plane scale (1 for BF16)
 };
 
 struct tvr_trace {
@@ -276,6 +286,9 @@ bool env_flag(const char* name) {
   return !(e && std::string(e) == "0");
 }
 bool prefix_share_enabled() { return env_flag("TVR_PREFIX_SHARE"); }
+// TVR_LIN_ENTRY=0 runs the entry layer of REPLACE_HEAD sites through the full
+// GEMM instead of lin_entry.hpp (the tests compare both).
+bool lin_entry_enabled() { return env_flag("TVR_LIN_ENTRY"); }
 
 // Activation format of the model's GEMM inputs (split.hpp).
 int act_fmt(const tvr_model* m) {
@@ -490,9 +503,99 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   return TVR_OK;
 }
 
+// The linearised entry layer's model constants (lin_entry.hpp) for the
+// current planar mode: per layer l = 1 .. L-2, Wsc = W1[l] W_O[l-1] on the
+// exact-product fp32 MFMA GEMM, its planes (X2F16: per-layer power-of-two
+// scale, as the weights), and c1[l] = row sums of W1[l] in fp64.
+int ensure_lin(tvr_model* m, hipStream_t st) {
+  const int fmt = act_fmt(m);
+  if (fmt == ACT_F32) return fail(TVR_ERR_INVALID, "lin entry: needs a planar GEMM mode");
+  if (m->lin_planes && m->lin_mode == m->gemm_mode) return TVR_OK;
+  const tvr_config& c = m->cfg;
+  const int L = c.n_layers, d = c.d_model, H = c.n_heads, dh = c.d_head, N = m->D1;
+  if (L < 3) return fail(TVR_ERR_INVALID, "lin entry: needs >= 3 layers");
+  TVR_HIP(hipStreamSynchronize(st));
+  if (m->lin_planes) TVR_HIP(hipFree(m->lin_planes));
+  if (m->lin_c1) TVR_HIP(hipFree(m->lin_c1));
+  m->lin_planes = nullptr;
+  m->lin_c1 = nullptr;
+  const int KP = (dh + 31) / 32 * 32, npl = fmt == ACT_X2F16 ? 2 : 1;
+  const size_t per = (size_t)H * N * KP;
+  float *wt = nullptr, *sc = nullptr;
+  unsigned* d_max = nullptr;
+  auto cleanup = [&]() {
+    if (wt) (void)hipFree(wt);
+    if (sc) (void)hipFree(sc);
+    if (d_max) (void)hipFree(d_max);
+  };
+  if (hipMalloc(&m->lin_planes, (size_t)(L - 2) * npl * per * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&m->lin_c1, (size_t)L * N * sizeof(float)) != hipSuccess ||
+      hipMalloc(&wt, (size_t)d * d * sizeof(float)) != hipSuccess ||
+      hipMalloc(&sc, (size_t)N * d * sizeof(float)) != hipSuccess ||
+      hipMalloc(&d_max, sizeof(unsigned)) != hipSuccess) {
+    (void)hipGetLastError();
+    cleanup();
+    if (m->lin_planes) (void)hipFree(m->lin_planes);
+    if (m->lin_c1) (void)hipFree(m->lin_c1);
+    m->lin_planes = nullptr;
+    m->lin_c1 = nullptr;
+    return fail(TVR_ERR_NOMEM, "lin entry: the W1 W_O planes do not fit");
+  }
+  m->lin_scale.assign(L, 1.0f);
+  int rc = TVR_OK;
+  for (int l = 1; l <= L - 2 && rc == TVR_OK; ++l) {
+    hipLaunchKernelGGL(transpose_kernel, dim3((d + 31) / 32, (d + 31) / 32), dim3(32, 8), 0, st,
+                       m->layers[l - 1].w2, m->K2, wt, d);
+    GemmEpi e{};
+    e.out0 = sc;
+    e.ld0 = d;
+    rc = launch_gemm(EPI_BIAS, m->layers[l].w1, d, ACT_F32, MatW{wt}, d, N, d, d, e, st);
+    if (rc != TVR_OK) break;
+    float scale = 1.0f;
+    if (fmt == ACT_X2F16) {
+      unsigned hm = 0;
+      hipError_t e2 = hipMemsetAsync(d_max, 0, sizeof(unsigned), st);
+      if (e2 == hipSuccess) {
+        hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, sc, (size_t)N * d, d_max);
+        e2 = hipGetLastError();
+      }
+      if (e2 == hipSuccess) e2 = hipMemcpyAsync(&hm, d_max, sizeof(unsigned), hipMemcpyDeviceToHost, st);
+      if (e2 == hipSuccess) e2 = hipStreamSynchronize(st);
+      if (e2 != hipSuccess) {
+        rc = fail(TVR_ERR_HIP, std::string("lin entry: ") + hipGetErrorString(e2));
+        break;
+      }
+      float v;
+      std::memcpy(&v, &hm, sizeof(v));
+      scale = x2_weight_scale(v);
+      hipLaunchKernelGGL(lin_planes_kernel<ACT_X2F16>, dim3(4096), dim3(256), 0, st, sc, N, H, dh, KP, scale,
+                         m->lin_planes + (size_t)(l - 1) * npl * per);
+    } else {
+      hipLaunchKernelGGL(lin_planes_kernel<ACT_BF16>, dim3(4096), dim3(256), 0, st, sc, N, H, dh, KP, 1.0f,
+                         m->lin_planes + (size_t)(l - 1) * npl * per);
+    }
+    m->lin_scale[l] = scale;
+    hipLaunchKernelGGL(rowsum_kernel, dim3((N + 3) / 4), dim3(256), 0, st, m->layers[l].w1, N, d,
+                       m->lin_c1 + (size_t)l * N);
+    if (hipGetLastError() != hipSuccess) rc = fail(TVR_ERR_HIP, "lin entry: plane build launch failed");
+  }
+  if (rc == TVR_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(TVR_ERR_HIP, "lin entry: build failed");
+  cleanup();
+  if (rc != TVR_OK) {
+    (void)hipFree(m->lin_planes);
+    (void)hipFree(m->lin_c1);
+    m->lin_planes = nullptr;
+    m->lin_c1 = nullptr;
+    return rc;
+  }
+  m->lin_kp = KP;
+  m->lin_mode = m->gemm_mode;
+  return TVR_OK;
+}
+
 // y: fp32 [rows][ldy] (ACT_F32) or a planar activation format
 int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
-                 int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr) {
+                 int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr, float2* stats = nullptr) {
   if (rows <= 0) return TVR_OK;
   ProfSpan ps(m, st);
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
@@ -500,11 +603,11 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
   if (fmt == ACT_X2F16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
   else if (fmt == ACT_BF16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
   else
-    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
   TVR_HIP(hipGetLastError());
   // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B, bf16 2 B per element)
   ps.done(TVR_HBM_LNPRE, (double)rows * d * (4.0 + (fmt == ACT_BF16 ? 2.0 : 4.0)));
@@ -818,6 +921,8 @@ int tvr_model_destroy(tvr_model* m) {
   if (m->rot_sin) (void)hipFree(m->rot_sin);
   if (m->d_w2s) (void)hipFree(m->d_w2s);
   if (m->planes) (void)hipFree(m->planes);
+  if (m->lin_planes) (void)hipFree(m->lin_planes);
+  if (m->lin_c1) (void)hipFree(m->lin_c1);
   if (m->range_flag) (void)hipFree(m->range_flag);
   if (m->ws) (void)hipFree(m->ws);
   if (m->splitk_ws) (void)hipFree(m->splitk_ws);
@@ -853,6 +958,11 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   m->wu = MatW{m->wu.f};
   if (m->planes) TVR_HIP(hipFree(m->planes));
   m->planes = nullptr;
+  if (m->lin_planes) TVR_HIP(hipFree(m->lin_planes));
+  if (m->lin_c1) TVR_HIP(hipFree(m->lin_c1));
+  m->lin_planes = nullptr;
+  m->lin_c1 = nullptr;
+  m->lin_mode = -1;
   m->gemm_mode = TVR_GEMM_F32;
   if (mode == TVR_GEMM_F32) return TVR_OK;
 
@@ -1443,6 +1553,53 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   if (fused && !trace->p_targets.empty()) clean_tg = trace->p_targets;
   const int ktop = std::max(topk, fused ? trace->p_k : 0);
 
+  // Linearised entry layers (lin_entry.hpp): layer l in [1, L-2] of a fused
+  // sweep whose entering sites are all REPLACE_HEAD computes its entering
+  // rows' QKV + MLP-in outputs from the clean rows' (this sweep's rows
+  // [0, Rc)) and a K = d_head GEMM.  Tables per such layer: the distinct
+  // vectors (rows of G), the entering rows grouped by head, m-blocks of <= 64
+  // rows of one head.
+  const int fmt0 = act_fmt(m);
+  std::vector<char> use_lin(L, 0);
+  std::vector<int32_t> lin_vids;
+  std::vector<LinRow> lin_rows;
+  std::vector<LinMB> lin_mbs;
+  std::vector<int> lin_vid_off(L, 0), lin_nv(L, 0), lin_mb_off(L, 0), lin_nmb(L, 0), lin_nrows(L, 0);
+  int lin_max_nv = 0;
+  if (fused && fmt0 != ACT_F32 && L >= 3 && lin_entry_enabled()) {
+    for (int l = 1; l <= L - 2; ++l) {
+      const int k0 = cnt_le[l - 1], k1 = cnt_le[l];
+      bool ok = k1 > k0;
+      for (int k = k0; k < k1 && ok; ++k) ok = sites[order[k]].kind == TVR_SITE_REPLACE_HEAD_ALLPOS;
+      if (!ok) continue;
+      use_lin[l] = 1;
+      std::map<int, int> vrow;
+      lin_vid_off[l] = (int)lin_vids.size();
+      for (int k = k0; k < k1; ++k)
+        if (vrow.emplace(sites[order[k]].vec, (int)vrow.size()).second) lin_vids.push_back(sites[order[k]].vec);
+      lin_nv[l] = (int)vrow.size();
+      lin_max_nv = std::max(lin_max_nv, lin_nv[l]);
+      lin_mb_off[l] = (int)lin_mbs.size();
+      const int r_first = (int)lin_rows.size();
+      for (int h = 0; h < c.n_heads; ++h) {
+        const int g0 = (int)lin_rows.size();
+        for (int k = k0; k < k1; ++k) {
+          const int i = order[k];
+          const tvr_site& s = sites[i];
+          if (s.head != h) continue;
+          for (int q = 0; q < nrow[i]; ++q)
+            lin_rows.push_back(LinRow{Rc + row0[i] + q, trace->seq_off[s.seq] + p0[i] + q, vrow[s.vec], 0});
+        }
+        for (int r = g0; r < (int)lin_rows.size(); r += 64)
+          lin_mbs.push_back(LinMB{r, std::min(64, (int)lin_rows.size() - r), h, 0});
+      }
+      lin_nmb[l] = (int)lin_mbs.size() - lin_mb_off[l];
+      lin_nrows[l] = (int)lin_rows.size() - r_first;
+    }
+  }
+  const bool any_lin = !lin_mbs.empty();
+  if (any_lin) TVR_TRY(ensure_lin(m, st));
+
   const int RA = Rc + R;  // rows of the activation buffers
   const int FC = std::min(kFinalChunk, std::max(n_sites, nc));
   Carve cv;
@@ -1455,12 +1612,20 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const size_t o_clast = cv.take<int32_t>(nc);
   const size_t o_ctg = cv.take<int32_t>(nc);
   const size_t o_ctok = cv.take<int32_t>(Rc);
+  // (uploaded tables first: flush_uploads sends one span from the first to the last)
+  const size_t o_lin_rows = cv.take<LinRow>(lin_rows.size());
+  const size_t o_lin_mbs = cv.take<LinMB>(lin_mbs.size());
+  const size_t o_lin_vids = cv.take<int32_t>(lin_vids.size());
   const size_t o_resid = cv.take<float>((size_t)RA * d);
   const size_t o_xn = cv.take<float>((size_t)RA * d);
   const size_t o_qkv = cv.take<float>((size_t)RA * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)RA * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
   const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, ktop, out_logits));
+  const size_t o_lnstats = cv.take<float2>(any_lin ? RA : 0);
+  const size_t o_raw = cv.take<float>(any_lin ? (size_t)Rc * c.d_mlp : 0);
+  const size_t o_vact = cv.take<float>(any_lin ? (size_t)n_vectors * d : 0);  // vectors in the activation format
+  const size_t o_g = cv.take<float>((size_t)lin_max_nv * m->D1);
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -1474,6 +1639,11 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     ub.add(o_clast, clean_last);
     ub.add(o_ctg, clean_tg);
     ub.add(o_ctok, std::vector<int32_t>(trace->tokens.begin(), trace->tokens.begin() + Rc));
+  }
+  if (any_lin) {
+    ub.add(o_lin_rows, lin_rows);
+    ub.add(o_lin_mbs, lin_mbs);
+    ub.add(o_lin_vids, lin_vids);
   }
   TVR_TRY(flush_uploads(m, st, base, ub));
 
@@ -1510,6 +1680,64 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     return TVR_OK;
   };
 
+  float2* lnstats = (float2*)(base + o_lnstats);
+  float* raw_h = (float*)(base + o_raw);
+  uint16_t* vact = (uint16_t*)(base + o_vact);
+  if (any_lin) {
+    const size_t n = (size_t)n_vectors * d;
+    const dim3 g((unsigned)std::min<size_t>((n + 255) / 256, 8192));
+    if (fmt == ACT_X2F16)
+      hipLaunchKernelGGL(act_rows_kernel<ACT_X2F16>, g, dim3(256), 0, st, vectors, d, vact, n_vectors, d,
+                         m->range_flag);
+    else
+      hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, g, dim3(256), 0, st, vectors, d, vact, n_vectors, d,
+                         m->range_flag);
+    TVR_HIP(hipGetLastError());
+  }
+  // layer l's block with the linearised entry rows [Rp, Rl) (use_lin[l])
+  auto run_block_lin = [&](int l, int Rl, const float* cache, float* zf) -> int {
+    const tvr_layer_weights& w = m->layers[l];
+    const int Rp = Rc + rows_le[l - 1], D1 = m->D1;
+    TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, Rl, d, c.ln_eps, fmt, st, m, lnstats));
+    GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);
+    e1.raw = raw_h;
+    e1.raw_rows = Rc;
+    e1.ld_raw = c.d_mlp;
+    TVR_TRY(launch_gemm(EPI_SPLIT_GELU_ACT, a.xn, d, fmt, m->w1[l], d, Rp, D1, d, e1, st, m));
+    ProfSpan ps(m, st);
+    const bool prof = m->prof;
+    m->prof = false;  // G and the entry rows are timed as one HBM-kind span, not as GEMM-family launches
+    GemmEpi eg{};
+    eg.out0 = (float*)(base + o_g);
+    eg.ld0 = D1;
+    eg.a_rows = (const int32_t*)(base + o_lin_vids) + lin_vid_off[l];
+    int rc = launch_gemm(EPI_BIAS, vact, d, fmt, m->w1[l], d, lin_nv[l], D1, d, eg, st, m);
+    m->prof = prof;
+    TVR_TRY(rc);
+    const int npl = fmt == ACT_X2F16 ? 2 : 1, KP = m->lin_kp;
+    const size_t per = (size_t)c.n_heads * D1 * KP;
+    const uint16_t* wp = m->lin_planes + (size_t)(l - 1) * npl * per;
+    const float acc_scale = fmt == ACT_X2F16 ? 1.0f / (m->lin_scale[l] * X2_ASCALE) : 1.0f;
+    const dim3 g(lin_nmb[l], (D1 + 255) / 256);
+#define TVR_LIN(F)                                                                                                 \
+  hipLaunchKernelGGL(lin_entry_kernel<F>, g, dim3(LIN_THREADS), 0, st, (const LinMB*)(base + o_lin_mbs) + lin_mb_off[l], \
+                     (const LinRow*)(base + o_lin_rows), wp, per, KP, acc_scale, trace->z + (size_t)(l - 1) * tstride, \
+                     d, c.d_head, lnstats, a.qkv, raw_h, c.d_mlp, (const float*)(base + o_g), m->lin_c1 + (size_t)l * D1, \
+                     w.b1, D1, reinterpret_cast<uint16_t*>(a.a2) + d, 2 * m->K2, m->K2, m->range_flag)
+    if (fmt == ACT_X2F16) TVR_LIN(ACT_X2F16); else TVR_LIN(ACT_BF16);
+#undef TVR_LIN
+    TVR_HIP(hipGetLastError());
+    // algorithmic bytes: the entering rows' outputs written and their clean rows' y_c read (4 B per
+    // column each), z slices, the layer's Wsc planes once, G written + read, the vectors' planes
+    const double nr = lin_nrows[l];
+    ps.done(TVR_HBM_LIN_ENTRY, nr * (8.0 * D1 + 4.0 * c.d_head) + 2.0 * npl * per +
+                                   lin_nv[l] * (8.0 * D1 + 4.0 * d) + 2.0 * npl * (double)D1 * d);
+    ProfSpan pa(m, st);
+    TVR_TRY(launch_attention(m, a.qkv, cache, d_seqs, nc + cnt_le[l], maxT, a.a2, a.fmt, zf, st, false, Rc));
+    pa.done(TVR_HBM_ATTENTION, attention_bytes(d, Rl, Rl, a.fmt, zf ? std::min(Rl, Rc) : 0));
+    return run_block_out(m, l, Rl, a, st);
+  };
+
   for (int l = 0; l < L; ++l) {
     if (fused)  // hook_resid_pre of the clean rows (the entries below read it from the trace)
       TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, rbytes, hipMemcpyDeviceToDevice, st));
@@ -1519,7 +1747,9 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     float* tqkv = trace->qkv + (size_t)l * 3 * tstride;
     const float* cache = fused ? a.qkv : tqkv;
     float* zf = fused ? trace->z + l * tstride : nullptr;  // the clean rows' hook_z (rows < Rc)
-    if (l == L - 1) {
+    if (use_lin[l]) {
+      TVR_TRY(run_block_lin(l, Rl, cache, zf));
+    } else if (l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), nc + cnt_le[l], maxT, a, cache,
                                   (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc));
     } else {

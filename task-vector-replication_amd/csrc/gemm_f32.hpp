@@ -93,6 +93,12 @@ struct GemmEpi {
   int stats_tiles;
   const int32_t* targets;
   float* tlogit;
+  // EPI_SPLIT_GELU_ACT: rows m < raw_rows also store their GELU columns'
+  // pre-activation (fp32, bias added) at raw + m * ld_raw + (c - n_split) — the
+  // clean rows' y_c that lin_entry.hpp reads in the same sweep.
+  float* raw;
+  int raw_rows;
+  int ld_raw;
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":
@@ -156,10 +162,12 @@ __device__ __forceinline__ void epi_store(const GemmEpi& ep, size_t orow, int co
     else
       ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
   } else if constexpr (EPI == EPI_SPLIT_GELU_ACT) {
-    if (col < ep.n_split)
+    if (col < ep.n_split) {
       ep.out0[orow * ep.ld0 + col] = v;
-    else
+    } else {
+      if (ep.raw && orow < (size_t)ep.raw_rows) ep.raw[orow * ep.ld_raw + (col - ep.n_split)] = v;
       store_act<FMT>(ep.out1h + orow * ep.ld1h + (col - ep.n_split), ep.ps1h, gelu_erf(v), ep.range_flag);
+    }
   } else {
     ep.out0[orow * ep.ld0 + col] = v + ep.resid[orow * ep.ldr + col];
   }

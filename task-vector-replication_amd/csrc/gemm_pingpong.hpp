@@ -168,13 +168,18 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
         const f32x4 x0 = *(const f32x4*)src, x1 = *(const f32x4*)(src + 4);
         float v[8] = {x0[0] + b8[0], x0[1] + b8[1], x0[2] + b8[2], x0[3] + b8[3],
                       x1[0] + b8[4], x1[1] + b8[5], x1[2] + b8[6], x1[3] + b8[7]};
+        const int m = row0 + p * 128 + r;
+        if (ep.raw && m < ep.raw_rows) {  // the clean rows' pre-GELU values (lin_entry.hpp)
+          float* q = ep.raw + (size_t)m * ep.ld_raw + (col0 + c8 - ep.n_split);
+          *(f32x4*)q = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)(q + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
 #pragma unroll
         for (int k = 0; k < 8; k += 2) {
           const f32x2 g = gelu_erf2(f32x2{v[k], v[k + 1]});
           v[k] = g.x;
           v[k + 1] = g.y;
         }
-        const int m = row0 + p * 128 + r;
         const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
         if (!NOSTORE || v[0] == 1.2345e-30f)  // NOSTORE (diagnostic): the LDS pass and math without the stores
           store_act8<FMT, PP_NT_STORES>(ep.out1h + orow * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v, ep.range_flag);

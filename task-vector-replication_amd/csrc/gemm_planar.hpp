@@ -91,6 +91,7 @@ __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n
     if (n0 < ep.n_split) {  // n_split % 4 == 0: a group never straddles it
       st16<NT>(ep.out0 + orow * ep.ld0 + n0, v);
     } else {
+      if (ep.raw && orow < (size_t)ep.raw_rows) st16<false>(ep.raw + orow * ep.ld_raw + (n0 - ep.n_split), v);
       const f32x2 g01 = gelu_erf2(f32x2{v[0], v[1]}), g23 = gelu_erf2(f32x2{v[2], v[3]});
       store_act4<FMT>(ep.out1h + orow * ep.ld1h + (n0 - ep.n_split), ep.ps1h, g01.x, g01.y, g23.x, g23.y,
                       ep.range_flag);

@@ -72,7 +72,7 @@ template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
                              void* __restrict__ y, int ldy, int rows, int d,
-                             float eps) {
+                             float eps, float2* __restrict__ stats) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;
@@ -99,6 +99,7 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
       }
     }
     const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
+    if (stats && lane == 0) stats[r] = make_float2(mean, scale);
 #pragma unroll
     for (int u = 0; u < LN_REG_F4; ++u) {
       if (u < nv) {
@@ -126,6 +127,7 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     ss += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
   }
   const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
+  if (stats && lane == 0) stats[r] = make_float2(mean, scale);
   for (int c = lane; c < d4; c += 64) {
     float4 v = xr[c];
     v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;

@@ -1,0 +1,205 @@
+// lin_entry.hpp — the first layer after a head-replacement patch, linearised.
+//
+// A REPLACE_HEAD_ALLPOS site (layer l-1, head h, vector v) enters the
+// staircase at layer l with, at every position,
+//     r = r_c + v - z_h W_O[h]            (entry_kernel; r_c the clean row)
+// and layer l's QKV + MLP-in GEMM reads LNPre(r) = (r - mu) / sigma, so
+//     y = LNPre(r) W1^T = (r W1^T - mu c1) / sigma,      c1[n] = sum_j W1[n][j]
+// Every term of r W1^T is already known or cheap:
+//     r_c W1^T = sigma_c y_c + mu_c c1     (y_c: the clean row's own GEMM output
+//                                           at layer l, computed in the same sweep)
+//     v W1^T   = G[v]                      (one [n_vectors] x d GEMM per layer)
+//     z_h W_O[h] W1^T = z_h Wsc[h]         (Wsc = W1[l] W_O[l-1]: [D1][H dh],
+//                                           a model constant, K = d_head)
+// so the entering rows' K = d_model GEMM (2 d D1 FLOP per row) becomes a
+// K = d_head one (2 d_head D1): 32x less work at 2.8B, the same fp32-accurate
+// arithmetic (x2f16 split, 3 products; the sums above are exact algebra, each
+// term carries fp32-level rounding).  Only the QKV + MLP-in GEMM of the ENTRY
+// layer is linear in the patch: attention and GELU are not, so layers > l run
+// in full.  The reference computes every such row with a full batch-1
+// forward (scratch2.py:181-194).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gemm_planar.hpp"
+
+namespace tvr {
+
+// One block's rows: entering rows [row0, row0 + rows) of the layer's row list
+// (rows <= 64), all of head `head`.
+struct LinMB {
+  int row0, rows, head, pad;
+};
+// One entering row: its activation row, its clean row (trace row of the same
+// prompt position: y_c, z_h and the clean LN statistics) and its vector's row of G.
+struct LinRow {
+  int out_row, clean_row, vrow, pad;
+};
+
+constexpr int LIN_THREADS = 256;  // 4 waves, each 64 rows x 64 columns of a 64 x 256 tile
+
+// out[n][j] = in[j * ldi + n] for n, j < d (the W_O block of w2, transposed: load time)
+__global__ void transpose_kernel(const float* __restrict__ in, int ldi, float* __restrict__ out, int d) {
+  __shared__ float t[32][33];
+  const int j0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  for (int r = threadIdx.y; r < 32; r += blockDim.y)
+    if (j0 + r < d && n0 + threadIdx.x < d) t[r][threadIdx.x] = in[(size_t)(j0 + r) * ldi + n0 + threadIdx.x];
+  __syncthreads();
+  for (int r = threadIdx.y; r < 32; r += blockDim.y)
+    if (n0 + r < d && j0 + threadIdx.x < d) out[(size_t)(n0 + r) * d + j0 + threadIdx.x] = t[threadIdx.x][r];
+}
+
+// c1[n] = sum_j w[n][j] (fp64 accumulation, one wave per row: load time)
+__global__ void rowsum_kernel(const float* __restrict__ w, int n_rows, int k, float* __restrict__ c1) {
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  double s = 0.0;
+  for (int j = lane; j < k; j += 64) s += (double)w[(size_t)row * k + j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) c1[row] = (float)s;
+}
+
+// Wsc fp32 [N][H dh] -> planes [NPL][H][N][KP] (head-major, k zero-padded to
+// KP): X2F16 two fp16 planes of w * scale (as the model's weight planes),
+// BF16 one bf16 plane.
+template <int FMT>
+__global__ void lin_planes_kernel(const float* __restrict__ s, int N, int H, int dh, int KP, float scale,
+                                  uint16_t* __restrict__ out) {
+  const size_t n_out = (size_t)H * N * KP;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_out; i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % KP);
+    const size_t hn = i / KP;
+    const int n = (int)(hn % N), h = (int)(hn / N);
+    const float w = k < dh ? s[(size_t)n * H * dh + h * dh + k] : 0.0f;
+    if constexpr (FMT == ACT_X2F16) {
+      const float x = w * scale;
+      const _Float16 h0 = (_Float16)x;
+      out[i] = __builtin_bit_cast(uint16_t, h0);
+      out[n_out + i] = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)h0));
+    } else {
+      out[i] = bf16_bits(w);
+    }
+  }
+}
+
+// The entering rows' QKV + MLP-in outputs (see the file comment).  Block
+// (m-block b, column tile c): rows of mbs[b] x columns [256 c, 256 c + 256);
+// wave w takes columns 64 w .. 64 w + 63 as 4 x 4 accumulators of 16 x 16,
+// D = Wsc z^T on v_mfma_f32_16x16x32_{f16,bf16} (lane l ends with four
+// consecutive columns of row l & 15, as gemm_planar.hpp).  z (fp32, the clean
+// run's hook_z at layer l-1) is split in registers: 16 z = z0 + z1 (X2F16),
+// products z0 w0 + z0 w1 + z1 w0.  The tile then goes through LDS so that the
+// combine reads y_c and stores its outputs as whole 1-KB rows (4 consecutive
+// columns per thread): per element
+//     y = (sigma_c (y_c - b1) + (mu_c - mu) c1 + G[v] - z_h Wsc[h]) / sigma + b1
+// (y_c = the clean row's qkv, or its pre-GELU MLP-in value raw_h), stored as
+// the QKV + MLP-in epilogue does: Q|K|V fp32 to qkv, GELU(h) in the
+// activation format to the a2 columns after z.
+constexpr int LIN_LDR = 260;  // floats per LDS row (conflict-free 16-B writes of the 16 x 16 fragments)
+template <int FMT>
+__global__ void __launch_bounds__(LIN_THREADS)
+lin_entry_kernel(const LinMB* __restrict__ mbs, const LinRow* __restrict__ rows, const uint16_t* __restrict__ wp,
+                 size_t wps, int KP, float acc_scale, const float* __restrict__ z, int d, int dh,
+                 const float2* __restrict__ stats, float* __restrict__ qkv, const float* __restrict__ raw_h,
+                 int d_mlp, const float* __restrict__ G, const float* __restrict__ c1, const float* __restrict__ b1,
+                 int N, uint16_t* __restrict__ out1h, int ld1h, int ps1h, unsigned* __restrict__ range_flag) {
+  using frag = typename PlanarFmt<FMT>::frag;
+  __shared__ __attribute__((aligned(16))) float tile[64 * LIN_LDR];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col0 = blockIdx.y * 256, nb = col0 + wave * 64;
+  const LinMB mb = mbs[blockIdx.x];
+  const int r16 = lane & 15, g = lane >> 4;
+  if (nb < N) {  // (a wave past N skips the product but joins the barrier)
+    int zrow[4];
+    bool live[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      live[i] = 16 * i + r16 < mb.rows;
+      zrow[i] = rows[mb.row0 + (live[i] ? 16 * i + r16 : 0)].clean_row;
+    }
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+    const uint16_t* wh = wp + (size_t)mb.head * N * KP;
+    for (int ks = 0; ks < KP; ks += 32) {
+      const int k = ks + 8 * g;  // this lane's 8 k values (dh % 16 == 0: a chunk is wholly in or out)
+      frag a0[4], a1[4], w0[4], w1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 x = {}, y = {};
+        if (live[i] && k < dh) {
+          const float* zr = z + (size_t)zrow[i] * d + mb.head * dh + k;
+          x = *(const f32x4*)zr;
+          y = *(const f32x4*)(zr + 4);
+        }
+        const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if constexpr (FMT == ACT_X2F16) {
+            const float s16 = v[e] * X2_ASCALE;
+            const _Float16 h0 = (_Float16)s16;
+            a0[i][e] = h0;
+            a1[i][e] = (_Float16)(s16 - (float)h0);
+          } else {
+            a0[i][e] = (__bf16)v[e];
+          }
+        }
+      }  // (z's X2F16 range was checked by its producer, the attention kernel)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = min(nb + 16 * j + r16, N - 1);
+        const uint16_t* p = wh + (size_t)n * KP + k;
+        w0[j] = *(const frag*)p;
+        if constexpr (FMT == ACT_X2F16) w1[j] = *(const frag*)(p + wps);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 c = acc[i][j];
+          if constexpr (FMT == ACT_X2F16) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[j], a1[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[j], a0[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[j], a0[i], c, 0, 0, 0);
+          } else {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], a0[i], c, 0, 0, 0);
+          }
+          acc[i][j] = c;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(f32x4*)(tile + (16 * i + r16) * LIN_LDR + wave * 64 + 16 * j + 4 * g) = acc[i][j] * acc_scale;
+  }
+  __syncthreads();
+  // combine + store: thread t takes columns col0 + 4 (t & 63) .. +3 of rows t >> 6, + 4, ...
+  const int cl = 4 * (threadIdx.x & 63), n0 = col0 + cl, n3 = 3 * d;
+  if (n0 >= N) return;
+  const f32x4 b = *(const f32x4*)(b1 + n0), c = *(const f32x4*)(c1 + n0);
+  for (int r = threadIdx.x >> 6; r < mb.rows; r += LIN_THREADS / 64) {
+    const LinRow q = rows[mb.row0 + r];
+    const float2 st = stats[q.out_row], sc = stats[q.clean_row];
+    const float dmu = sc.x - st.x;
+    const f32x4 v = *(const f32x4*)(tile + r * LIN_LDR + cl);
+    const f32x4 yc = n0 < n3 ? *(const f32x4*)(qkv + (size_t)q.clean_row * n3 + n0)
+                             : *(const f32x4*)(raw_h + (size_t)q.clean_row * d_mlp + (n0 - n3));
+    const f32x4 gv = *(const f32x4*)(G + (size_t)q.vrow * N + n0);
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (sc.y * (yc[e] - b[e]) + dmu * c[e] + gv[e] - v[e]) / st.y + b[e];
+    if (n0 < n3) {
+      *(f32x4*)(qkv + (size_t)q.out_row * n3 + n0) = y;
+    } else {
+      const f32x2 g01 = gelu_erf2(f32x2{y[0], y[1]}), g23 = gelu_erf2(f32x2{y[2], y[3]});
+      store_act4<FMT>(out1h + (size_t)q.out_row * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
+    }
+  }
+}
+
+}  // namespace tvr
