@@ -1718,13 +1718,20 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     const size_t per = (size_t)c.n_heads * D1 * KP;
     const uint16_t* wp = m->lin_planes + (size_t)(l - 1) * npl * per;
     const float acc_scale = fmt == ACT_X2F16 ? 1.0f / (m->lin_scale[l] * X2_ASCALE) : 1.0f;
-    const dim3 g(lin_nmb[l], (D1 + 255) / 256);
-#define TVR_LIN(F)                                                                                                 \
-  hipLaunchKernelGGL(lin_entry_kernel<F>, g, dim3(LIN_THREADS), 0, st, (const LinMB*)(base + o_lin_mbs) + lin_mb_off[l], \
-                     (const LinRow*)(base + o_lin_rows), wp, per, KP, acc_scale, trace->z + (size_t)(l - 1) * tstride, \
-                     d, c.d_head, lnstats, a.qkv, raw_h, c.d_mlp, (const float*)(base + o_g), m->lin_c1 + (size_t)l * D1, \
-                     w.b1, D1, reinterpret_cast<uint16_t*>(a.a2) + d, 2 * m->K2, m->K2, m->range_flag)
-    if (fmt == ACT_X2F16) TVR_LIN(ACT_X2F16); else TVR_LIN(ACT_BF16);
+    const dim3 g(lin_nmb[l] * ((D1 + 255) / 256));
+#define TVR_LIN(F, NK)                                                                                             \
+  hipLaunchKernelGGL((lin_entry_kernel<F, NK>), g, dim3(LIN_THREADS), 0, st,                                       \
+                     (const LinMB*)(base + o_lin_mbs) + lin_mb_off[l], lin_nmb[l], (const LinRow*)(base + o_lin_rows), \
+                     wp, per, acc_scale, trace->z + (size_t)(l - 1) * tstride, d, c.d_head, lnstats, a.qkv, raw_h,     \
+                     c.d_mlp, (const float*)(base + o_g), m->lin_c1 + (size_t)l * D1, w.b1, D1,                         \
+                     reinterpret_cast<uint16_t*>(a.a2) + d, 2 * m->K2, m->K2, m->range_flag)
+#define TVR_LIN_K(F)                                                      \
+  if (KP == 32) TVR_LIN(F, 1);                                            \
+  else if (KP == 64) TVR_LIN(F, 2);                                       \
+  else if (KP == 96) TVR_LIN(F, 3);                                       \
+  else TVR_LIN(F, 4)
+    if (fmt == ACT_X2F16) { TVR_LIN_K(ACT_X2F16); } else { TVR_LIN_K(ACT_BF16); }
+#undef TVR_LIN_K
 #undef TVR_LIN
     TVR_HIP(hipGetLastError());
     // algorithmic bytes: the entering rows' outputs written and their clean rows' y_c read (4 B per

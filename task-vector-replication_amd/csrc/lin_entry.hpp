@@ -94,49 +94,90 @@ __global__ void lin_planes_kernel(const float* __restrict__ s, int N, int H, int
 // combine reads y_c and stores its outputs as whole 1-KB rows (4 consecutive
 // columns per thread): per element
 //     y = (sigma_c (y_c - b1) + (mu_c - mu) c1 + G[v] - z_h Wsc[h]) / sigma + b1
+// (each row's sigma_c / sigma, (mu_c - mu) / sigma and 1 / sigma staged in LDS first)
 // (y_c = the clean row's qkv, or its pre-GELU MLP-in value raw_h), stored as
 // the QKV + MLP-in epilogue does: Q|K|V fp32 to qkv, GELU(h) in the
 // activation format to the a2 columns after z.
 constexpr int LIN_LDR = 260;  // floats per LDS row (conflict-free 16-B writes of the 16 x 16 fragments)
-template <int FMT>
+// NK = KP / 32 k-steps, fully unrolled with the next step's z / Wsc loads
+// issued before this step's MFMAs.  1-D grid of n_mb x column tiles with the
+// XCD-aware bijective remap (gemm_pingpong.hpp): the m-blocks that share a
+// head's Wsc tile are consecutive work items, so they run on one XCD together
+// and read that tile from one L2.
+template <int FMT, int NK>
 __global__ void __launch_bounds__(LIN_THREADS)
-lin_entry_kernel(const LinMB* __restrict__ mbs, const LinRow* __restrict__ rows, const uint16_t* __restrict__ wp,
-                 size_t wps, int KP, float acc_scale, const float* __restrict__ z, int d, int dh,
-                 const float2* __restrict__ stats, float* __restrict__ qkv, const float* __restrict__ raw_h,
+lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restrict__ rows,
+                 const uint16_t* __restrict__ wp, size_t wps, float acc_scale, const float* __restrict__ z, int d,
+                 int dh, const float2* __restrict__ stats, float* __restrict__ qkv, const float* __restrict__ raw_h,
                  int d_mlp, const float* __restrict__ G, const float* __restrict__ c1, const float* __restrict__ b1,
                  int N, uint16_t* __restrict__ out1h, int ld1h, int ps1h, unsigned* __restrict__ range_flag) {
   using frag = typename PlanarFmt<FMT>::frag;
+  constexpr int KP = 32 * NK;
   __shared__ __attribute__((aligned(16))) float tile[64 * LIN_LDR];
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int mbi = work % n_mb, ct = work / n_mb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int col0 = blockIdx.y * 256, nb = col0 + wave * 64;
-  const LinMB mb = mbs[blockIdx.x];
+  const int col0 = ct * 256, nb = col0 + wave * 64;
+  const LinMB mb = mbs[mbi];
   const int r16 = lane & 15, g = lane >> 4;
+  // per-row combine coefficients, staged while the product runs:
+  // y = A (y_c - b1) + B c1 + I (G[v] - z Wsc) + b1,  A = sigma_c / sigma, B = (mu_c - mu) / sigma, I = 1 / sigma
+  __shared__ f32x4 rcoef[64];
+  __shared__ int4 rrow[64];
+  if (threadIdx.x < mb.rows) {
+    const LinRow q = rows[mb.row0 + threadIdx.x];
+    const float2 st = stats[q.out_row], sc = stats[q.clean_row];
+    const float inv = 1.0f / st.y;
+    rcoef[threadIdx.x] = f32x4{sc.y * inv, (sc.x - st.x) * inv, inv, 0.f};
+    rrow[threadIdx.x] = make_int4(q.out_row, q.clean_row, q.vrow, 0);
+  }
   if (nb < N) {  // (a wave past N skips the product but joins the barrier)
-    int zrow[4];
+    const float* zr[4];
     bool live[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       live[i] = 16 * i + r16 < mb.rows;
-      zrow[i] = rows[mb.row0 + (live[i] ? 16 * i + r16 : 0)].clean_row;
+      zr[i] = z + (size_t)rows[mb.row0 + (live[i] ? 16 * i + r16 : 0)].clean_row * d + mb.head * dh + 8 * g;
     }
+    const uint16_t* wr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wr[j] = wp + ((size_t)mb.head * N + min(nb + 16 * j + r16, N - 1)) * KP + 8 * g;
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
-    const uint16_t* wh = wp + (size_t)mb.head * N * KP;
-    for (int ks = 0; ks < KP; ks += 32) {
-      const int k = ks + 8 * g;  // this lane's 8 k values (dh % 16 == 0: a chunk is wholly in or out)
-      frag a0[4], a1[4], w0[4], w1[4];
+    // raw loads of k-step s (lane: 8 k values at 32 s + 8 g; dh % 16 == 0: a chunk is wholly in or out)
+    f32x4 zx[2][4], zy[2][4];
+    frag w0[2][4], w1[2][4];
+    auto load = [&](int s, int b) {
+      const bool kin = 32 * s + 8 * g < dh;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        f32x4 x = {}, y = {};
-        if (live[i] && k < dh) {
-          const float* zr = z + (size_t)zrow[i] * d + mb.head * dh + k;
-          x = *(const f32x4*)zr;
-          y = *(const f32x4*)(zr + 4);
+        zx[b][i] = f32x4{};
+        zy[b][i] = f32x4{};
+        if (live[i] && kin) {
+          zx[b][i] = *(const f32x4*)(zr[i] + 32 * s);
+          zy[b][i] = *(const f32x4*)(zr[i] + 32 * s + 4);
         }
-        const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0[b][j] = *(const frag*)(wr[j] + 32 * s);
+        if constexpr (FMT == ACT_X2F16) w1[b][j] = *(const frag*)(wr[j] + 32 * s + wps);
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      const int b = s & 1;
+      if (s + 1 < NK) load(s + 1, b ^ 1);
+      frag a0[4], a1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v[8] = {zx[b][i][0], zx[b][i][1], zx[b][i][2], zx[b][i][3],
+                            zy[b][i][0], zy[b][i][1], zy[b][i][2], zy[b][i][3]};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if constexpr (FMT == ACT_X2F16) {
@@ -150,23 +191,16 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, const LinRow* __restrict__ rows,
         }
       }  // (z's X2F16 range was checked by its producer, the attention kernel)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = min(nb + 16 * j + r16, N - 1);
-        const uint16_t* p = wh + (size_t)n * KP + k;
-        w0[j] = *(const frag*)p;
-        if constexpr (FMT == ACT_X2F16) w1[j] = *(const frag*)(p + wps);
-      }
-#pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f32x4 c = acc[i][j];
           if constexpr (FMT == ACT_X2F16) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[j], a1[i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[j], a0[i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[j], a0[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[b][j], a1[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[b][j], a0[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[b][j], a0[i], c, 0, 0, 0);
           } else {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], a0[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[b][j], a0[i], c, 0, 0, 0);
           }
           acc[i][j] = c;
         }
@@ -182,22 +216,22 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, const LinRow* __restrict__ rows,
   const int cl = 4 * (threadIdx.x & 63), n0 = col0 + cl, n3 = 3 * d;
   if (n0 >= N) return;
   const f32x4 b = *(const f32x4*)(b1 + n0), c = *(const f32x4*)(c1 + n0);
+#pragma unroll 4
   for (int r = threadIdx.x >> 6; r < mb.rows; r += LIN_THREADS / 64) {
-    const LinRow q = rows[mb.row0 + r];
-    const float2 st = stats[q.out_row], sc = stats[q.clean_row];
-    const float dmu = sc.x - st.x;
+    const int4 q = rrow[r];
+    const f32x4 k = rcoef[r];
     const f32x4 v = *(const f32x4*)(tile + r * LIN_LDR + cl);
-    const f32x4 yc = n0 < n3 ? *(const f32x4*)(qkv + (size_t)q.clean_row * n3 + n0)
-                             : *(const f32x4*)(raw_h + (size_t)q.clean_row * d_mlp + (n0 - n3));
-    const f32x4 gv = *(const f32x4*)(G + (size_t)q.vrow * N + n0);
+    const f32x4 yc = n0 < n3 ? *(const f32x4*)(qkv + (size_t)q.y * n3 + n0)
+                             : *(const f32x4*)(raw_h + (size_t)q.y * d_mlp + (n0 - n3));
+    const f32x4 gv = *(const f32x4*)(G + (size_t)q.z * N + n0);
     f32x4 y;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = (sc.y * (yc[e] - b[e]) + dmu * c[e] + gv[e] - v[e]) / st.y + b[e];
+    for (int e = 0; e < 4; ++e) y[e] = k[0] * (yc[e] - b[e]) + k[1] * c[e] + k[2] * (gv[e] - v[e]) + b[e];
     if (n0 < n3) {
-      *(f32x4*)(qkv + (size_t)q.out_row * n3 + n0) = y;
+      *(f32x4*)(qkv + (size_t)q.x * n3 + n0) = y;
     } else {
       const f32x2 g01 = gelu_erf2(f32x2{y[0], y[1]}), g23 = gelu_erf2(f32x2{y[2], y[3]});
-      store_act4<FMT>(out1h + (size_t)q.out_row * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
+      store_act4<FMT>(out1h + (size_t)q.x * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
     }
   }
 }
