@@ -779,6 +779,13 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
 bool final_fused(const tvr_model* m, int fmt, const float* out_logits) {
   return fmt != ACT_F32 && !out_logits && m->cfg.d_vocab % 4 == 0;
 }
+// rows per unembed launch: the fused statistics keep ~200 records per row (no
+// [rows][V] logits), so a whole sweep's sites go in one launch (one partly
+// empty last round instead of one per 1,024 rows: 37 rounds instead of 52 at
+// C3); the logits paths keep 1,024-row chunks of [rows][V] scratch.
+int final_chunk(const tvr_model* m, int fmt, const float* out_logits) {
+  return final_fused(m, fmt, out_logits) ? 16384 : kFinalChunk;
+}
 // floats of run_final's scratch for chunks of fc rows
 size_t final_scratch_floats(const tvr_model* m, int fmt, int fc, int topk, const float* out_logits) {
   const int V = m->cfg.d_vocab;
@@ -792,9 +799,9 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
   const tvr_config& c = m->cfg;
   const int d = c.d_model, V = c.d_vocab;
   const bool fused = final_fused(m, fmt, out_logits);
-  const int tiles = (V + 255) / 256;
-  for (int s = 0; s < n; s += kFinalChunk) {
-    const int cn = std::min(kFinalChunk, n - s);
+  const int tiles = (V + 255) / 256, chunk = final_chunk(m, fmt, out_logits);
+  for (int s = 0; s < n; s += chunk) {
+    const int cn = std::min(chunk, n - s);
     TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m));
     if (fused) {
       float* part = scratch;
@@ -1225,7 +1232,7 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
     out_rows.resize(R);
     for (int r = 0; r < R; ++r) out_rows[r] = r;
   }
-  const int FC = std::min(kFinalChunk, n_out);
+  const int FC = std::min(final_chunk(m, act_fmt(m), out_logits), n_out);
   Carve cv;
   const size_t o_seqs = cv.take<SeqDesc>(n_seq);
   const size_t o_seqs_last = cv.take<SeqDesc>(n_seq);
@@ -1601,7 +1608,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   if (any_lin) TVR_TRY(ensure_lin(m, st));
 
   const int RA = Rc + R;  // rows of the activation buffers
-  const int FC = std::min(kFinalChunk, std::max(n_sites, nc));
+  // run_final chunks: the sites' (logits requested or not) and the fused clean rows' (never logits)
+  const int FCs = std::min(final_chunk(m, fmt0, out_logits), n_sites), FCc = std::min(final_chunk(m, fmt0, nullptr), nc);
   Carve cv;
   const size_t o_seqs = cv.take<SeqDesc>(nc + n_sites);
   const size_t o_seqs_last = cv.take<SeqDesc>(nc + n_sites);
@@ -1620,8 +1628,9 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const size_t o_xn = cv.take<float>((size_t)RA * d);
   const size_t o_qkv = cv.take<float>((size_t)RA * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)RA * m->K2);
-  const size_t o_xf = cv.take<float>((size_t)FC * d);
-  const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, ktop, out_logits));
+  const size_t o_xf = cv.take<float>((size_t)std::max(FCs, FCc) * d);
+  const size_t o_lg = cv.take<float>(std::max(final_scratch_floats(m, fmt0, FCs, ktop, out_logits),
+                                              final_scratch_floats(m, fmt0, FCc, ktop, nullptr)));
   const size_t o_lnstats = cv.take<float2>(any_lin ? RA : 0);
   const size_t o_raw = cv.take<float>(any_lin ? (size_t)Rc * c.d_mlp : 0);
   const size_t o_vact = cv.take<float>(any_lin ? (size_t)n_vectors * d : 0);  // vectors in the activation format
