@@ -350,6 +350,7 @@ def main():
             variants[name] = {"launches": v["launches"],
                               "achieved_tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2),
                               "avg_launch_ms": round(v["ms"] / v["launches"], 4),
+                              "alg_bytes_per_launch": round(v["bytes"] / v["launches"]),
                               "share_of_gemm_time": round(v["ms"] / fam["ms"], 4)}
     parallelism = ("single GPU" if world == 1 else
                    f"sites sharded by head mod {world} (same {args.prompts} prompts on every GPU), weights replicated, "
@@ -388,6 +389,8 @@ def main():
                            f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
             "traffic": traffic,
             "traffic_source": traffic_src,
+            "traffic_basis": (pmc or {}).get("basis"),
+            "traffic_ratio_to_alg": (pmc or {}).get("ratio_hbm_to_alg"),
             "mfma_util_rocprof": (pmc.get("mfma") or {}).get("all") if pmc else None,
             "algorithmic_bytes_per_launch": round(fam["bytes"] / max(fam["launches"], 1)),
             "launches_per_step": fam["launches"] // psteps,

@@ -21,7 +21,11 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-VARIANTS = {"0": "unembed", "1": "qkv_mlpin", "2": "o_mlpout", "3": "qkv_mlpin", "4": "unembed"}
+# epilogue template argument -> variant; EPI_BIAS dispatches are the split-K partial
+# launches of every GEMM (the reduce applies the real epilogue) and the
+# linearised entry layer's G GEMMs; the unembed is EPI_STATS
+VARIANTS = {"0": "bias_partials", "1": "qkv_mlpin", "2": "o_mlpout", "3": "qkv_mlpin", "4": "unembed"}
+MAIN = ("qkv_mlpin", "o_mlpout")  # the step's two big GEMMs (95 % of its time): traffic / ratio basis
 SIMDS = 1024  # 256 CUs x 4
 
 
@@ -68,7 +72,7 @@ def gemm_variant(name):
 
 
 # the HBM-bound kernels (bench.py hbm_kernels names)
-HBM_KERNELS = {"entry_kernel": "entry", "lnpre_kernel": "lnpre", "attention_mfma_kernel": "attention",
+HBM_KERNELS = {"lin_entry_kernel": "lin_entry", "entry_kernel": "entry", "lnpre_kernel": "lnpre", "attention_mfma_kernel": "attention",
                "stats_merge_kernel": "row_stats", "row_stats_kernel": "row_stats", "capture_partial_kernel": "capture",
                "capture_finish_kernel": "capture"}
 
@@ -117,7 +121,7 @@ def pmc(d):
     return rows
 
 
-def mfma_util(rows):
+def mfma_util(rows, fam_only=None):
     """MFMA utilisation of the GEMM dispatches: SQ_VALU_MFMA_BUSY_CYCLES (summed
     over every SIMD) / (SIMDs x shader cycles), shader cycles = GRBM_GUI_ACTIVE / 8
     (rocprofv3 sums it over the 8 XCDs; MI355X_MICROARCH.md DVFS note); the
@@ -126,7 +130,7 @@ def mfma_util(rows):
     by = {}
     for r in rows:
         gv = gemm_variant(r["Kernel_Name"])
-        if not gv:
+        if not gv or (fam_only and gv[0] != fam_only):
             continue
         d = by.setdefault((r["Dispatch_Id"], gv), {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -180,7 +184,18 @@ def main():
                         "total_ms": round(int(r["TotalDurationNs"]) / 1e6, 3),
                         "avg_ms": round(float(r["AverageNs"]) / 1e6, 4), "pct": round(float(r["Percentage"]), 2)})
     summary = {"command": a.cmd, "kernels": kernels[:20]}
-    gemm = [k for k in kernels if any(f in k["kernel"] for f in FAMILIES)]
+    # the profiled family: the GEMM kernel with the most time (a planar-mode run
+    # also launches the fp32 GEMM once per layer while it builds the linearised
+    # entry layer's W1 W_O constants, csrc/lin_entry.hpp: model set-up, excluded)
+    fam_ms = {}
+    for r in csv.DictReader(open(stats_csv)):
+        gv = gemm_variant(r["Name"])
+        if gv:
+            fam_ms[gv[0]] = fam_ms.get(gv[0], 0.0) + int(r["TotalDurationNs"]) / 1e6
+    main_fam = max(fam_ms, key=fam_ms.get) if fam_ms else None
+    summary["excluded_gemm_families_ms"] = {k: round(v, 3) for k, v in fam_ms.items() if k != main_fam}
+    gemm = [k for k, r in zip(kernels, csv.DictReader(open(stats_csv)))
+            if (gemm_variant(r["Name"]) or (None,))[0] == main_fam]
     tot_calls = sum(k["calls"] for k in gemm)
     summary["gemm_family"] = {"calls": tot_calls, "total_ms": round(sum(k["total_ms"] for k in gemm), 3),
                               "avg_ms": round(sum(k["total_ms"] for k in gemm) / max(tot_calls, 1), 4)}
@@ -188,8 +203,8 @@ def main():
         f, w = pmc(a.fetch), pmc(a.write)
         # the two passes are separate runs of the same deterministic command:
         # pair the i-th GEMM dispatch of one with the i-th of the other
-        fg = [r for r in f if gemm_variant(r["Kernel_Name"])]
-        wg = [r for r in w if gemm_variant(r["Kernel_Name"])]
+        fg = [r for r in f if (gemm_variant(r["Kernel_Name"]) or (None,))[0] == main_fam]
+        wg = [r for r in w if (gemm_variant(r["Kernel_Name"]) or (None,))[0] == main_fam]
         if len(fg) != len(wg):
             raise SystemExit(f"PMC passes saw {len(fg)} vs {len(wg)} GEMM dispatches")
         per, fams = {}, set()
@@ -202,24 +217,34 @@ def main():
             p = per.setdefault(VARIANTS[v], {"launches": 0, "hbm_bytes": 0.0})
             p["launches"] += 1
             p["hbm_bytes"] += hbm
-        n = sum(p["launches"] for p in per.values())
-        hbm = sum(p["hbm_bytes"] for p in per.values())
+        n = sum(per[k]["launches"] for k in MAIN if k in per)
+        hbm = sum(per[k]["hbm_bytes"] for k in MAIN if k in per)
         if len(fams) != 1:
             raise SystemExit(f"profiled command ran GEMM families {sorted(fams)}; profile one at a time")
         fam = fams.pop()
         pm = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag {a.tag}", "family": fam,
               "correction": "HBM bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count of 16-B/lane reads) + WRITE_SIZE x 1024",
+              "basis": "qkv_mlpin + o_mlpout dispatches (split-K partial dispatches and the unembed listed apart)",
               "hbm_bytes_per_launch": round(hbm / n), "launches": n,
               "variants": {k: {"launches": p["launches"], "hbm_bytes_per_launch": round(p["hbm_bytes"] / p["launches"])}
                            for k, p in per.items()}}
         if a.bench:
             b = json.loads(Path(a.bench).read_text())
-            alg = b["roofline"]["algorithmic_bytes_per_launch"]
-            pm["alg_bytes_per_launch"] = alg
+            bv = b["roofline"].get("variants", {})
+            if all(k in bv and "alg_bytes_per_launch" in bv[k] for k in MAIN if k in per):
+                alg = sum(bv[k]["alg_bytes_per_launch"] * per[k]["launches"] for k in MAIN if k in per) / n
+                for k in MAIN:
+                    if k in per:
+                        pm["variants"][k]["alg_bytes_per_launch"] = bv[k]["alg_bytes_per_launch"]
+                        pm["variants"][k]["ratio_hbm_to_alg"] = round(
+                            per[k]["hbm_bytes"] / per[k]["launches"] / bv[k]["alg_bytes_per_launch"], 2)
+            else:
+                alg = b["roofline"]["algorithmic_bytes_per_launch"]
+            pm["alg_bytes_per_launch"] = round(alg)
             pm["workload"] = b["config"]["workload"]
             pm["ratio_hbm_to_alg"] = round(hbm / n / alg, 2)
         if a.mfma:
-            pm["mfma"] = mfma_util(pmc(a.mfma))
+            pm["mfma"] = mfma_util(pmc(a.mfma), main_fam)
         summary["pmc_gemm"] = pm
         (out_dir / f"pmc_gemm_{fam}.json").write_text(json.dumps(pm, indent=1) + "\n")
         hk = hbm_kernel_traffic(f, w, json.loads(Path(a.bench).read_text()) if a.bench else None)
