@@ -158,11 +158,30 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
     }
     __syncthreads();
     const int rows = min(128, Mlim - p * 128);
+    // No global load may sit between two of a thread's row stores: s_waitcnt
+    // vmcnt counts loads and stores together in issue order, so waiting for a
+    // load issued after a store waits for that store to reach memory, and a
+    // per-row load (out_rows[m], the residual) turned the row loop into one
+    // store round trip per row.  The gathered row indices and the residual
+    // rows are therefore loaded for all of the thread's rows of the half
+    // before its first store (rows past `rows` read a valid row and store
+    // nothing): a half's stores wait for memory once per batch of rows at
+    // most (twice per GELU half), not once per row.
     if constexpr (EPI == EPI_STATS) {
       pp_stats_rows(ep, L, row0 + p * 128, col0, rows, Nlim, b4, t);
     } else if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
-#pragma unroll 2
-      for (int r = t >> 5; r < 128; r += PP_THREADS / 32) {
+      constexpr int RPT = 128 / (PP_THREADS / 32);  // rows per thread (8)
+      const int rb = t >> 5;
+      int orow[RPT];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) orow[i] = row0 + p * 128 + min(rb + i * (PP_THREADS / 32), max(rows - 1, 0));
+      if (ep.out_rows) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) orow[i] = ep.out_rows[orow[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int r = rb + i * (PP_THREADS / 32);
         if (r >= rows) break;
         const float* src = L + r * PP_EPI_LDR + c8;
         const f32x4 x0 = *(const f32x4*)src, x1 = *(const f32x4*)(src + 4);
@@ -180,19 +199,43 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
           v[k] = g.x;
           v[k + 1] = g.y;
         }
-        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
         if (!NOSTORE || v[0] == 1.2345e-30f)  // NOSTORE (diagnostic): the LDS pass and math without the stores
-          store_act8<FMT, PP_NT_STORES>(ep.out1h + orow * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v, ep.range_flag);
+          store_act8<FMT, PP_NT_STORES>(ep.out1h + (size_t)orow[i] * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v,
+                                        ep.range_flag);
       }
     } else if (c4 < Nlim) {
-#pragma unroll 4
-      for (int r = t >> 6; r < 128; r += PP_THREADS / 64) {
-        if (r >= rows) break;
-        const f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
-        const int m = row0 + p * 128 + r;
-        const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
-        if (!NOSTORE || v[0] == 1.2345e-30f)
-          epi_store4<EPI, FMT, PP_NT_STORES && EPI == EPI_SPLIT_GELU_ACT>(ep, orow, col0 + c4, v);
+      // 16 rows per thread, in two batches of 8: the residual rows of a batch
+      // (32 VGPRs; the waves of the other half still hold their accumulators)
+      // are loaded before its stores, so a half waits for memory twice, not
+      // once per row
+      constexpr int RB = 8, NB = 128 / (PP_THREADS / 64) / RB;
+      const int rb = t >> 6;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        int orow[RB];
+        f32x4 rr[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) orow[i] = row0 + p * 128 + min(rb + (b * RB + i) * (PP_THREADS / 64), max(rows - 1, 0));
+        if (ep.out_rows) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i) orow[i] = ep.out_rows[orow[i]];
+        }
+        if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i) rr[i] = *(const f32x4*)(ep.resid + (size_t)orow[i] * ep.ldr + col0 + c4);
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int r = rb + (b * RB + i) * (PP_THREADS / 64);
+          if (r >= rows) break;
+          f32x4 v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
+          if (!NOSTORE || v[0] == 1.2345e-30f) {
+            if constexpr (EPI == EPI_RESID)
+              st16<false>(ep.out0 + (size_t)orow[i] * ep.ld0 + col0 + c4, v + rr[i]);
+            else
+              epi_store4<EPI, FMT, PP_NT_STORES && EPI == EPI_SPLIT_GELU_ACT>(ep, orow[i], col0 + c4, v);
+          }
+        }
       }
     }
     __syncthreads();
@@ -393,6 +436,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       GemmEpi pe = ep;
       pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
       pe.ld0 = 256;
+      pe.out_rows = nullptr;  // partial tiles are stored densely; the reduce applies out_rows
       pp_epilogue_lds<EPI, FMT, VAR == 8>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
     } else {
       pp_epilogue_lds<EPI, FMT, VAR == 8>(ep, acc, L, m0, n0, M - m0, N - n0, wr, wc, lane, t, acc_scale);

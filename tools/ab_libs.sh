@@ -1,0 +1,16 @@
+# Same-box A/B of two in-tree engine builds on the default bench, interleaved
+# (A B A B ...: rule 24, one device), value lines to gpurun_out/ab_<tag>/.
+#   gpurun -- 'bash tools/ab_libs.sh <tag> <rounds> <libA.so> <libB.so> [extra bench args]'
+set -o pipefail
+TAG=${1:?tag}; ROUNDS=${2:?rounds}; LA=${3:?libA}; LB=${4:?libB}; shift 4
+export TMPDIR=/tmp
+OUT=gpurun_out/ab_$TAG
+mkdir -p $OUT
+for r in $(seq 1 $ROUNDS); do
+  for lib in $LA $LB; do
+    n=$(basename $lib .so)_$r
+    TVR_LIB=$lib timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-f32-leg --extract 0 "$@" \
+        > $OUT/$n.json 2> $OUT/$n.err || { tail -5 $OUT/$n.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; h=d.get('hbm_kernels') or {}; print(sys.argv[2], d['value'], d['ms_per_step'], r['achieved'], {k: v['achieved_tflops'] for k, v in r['variants'].items()})" $OUT/$n.json $n | tee -a $OUT/summary.txt
+  done
+done
