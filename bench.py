@@ -403,6 +403,11 @@ def main():
         "algorithmic": {
             "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(value * f_alg / 1e12, 2),
+            # BASELINE.md section 3's roofline fraction: the reference's algorithmic work per site
+            #  x sites/s over the whole timed step, against the same peak
+            # (work the engine skips -- shared prefixes, the trimmed last layer, the linearised
+            # entry layer -- counts as done, as in the reference's loop)
+            "site_frac": round(value * f_alg / 1e12 / peak, 4),
             "extraction_prompts_per_s": round(n_ex / te, 1) if te else None,
         },
     }
