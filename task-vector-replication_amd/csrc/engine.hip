@@ -25,6 +25,7 @@
 #include "gemm_f32.hpp"
 #include "attention_mfma.hpp"
 #include "gemm_pingpong.hpp"
+#include "gemm_skinny.hpp"
 #include "gemm_planar.hpp"
 #include "gemm_x2f16.hpp"
 #include "gemm_x3bf16.hpp"
@@ -443,17 +444,35 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   if (planar) {
     const uint16_t* Ah = static_cast<const uint16_t*>(A);
     const bool vec = planar_epilogue_vec(epi, ep, N);
-    PpPlan plan;
-    if (m && vec && epi != EPI_STATS) plan = plan_pp(M, N, K, a_fmt);
-    if (plan.ksplit > 1) {
-      TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, gemm_pingpong_grid(M, N),
-                               plan.ksplit, m, st));
-    } else if (plan.tail_base > 0) {
-      launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, true, st);
-      TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
-                               gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st));
+    if (ep.skinny && epi == EPI_BIAS && M <= SK_MAX_M && !ep.out_rows && ep.k_split <= 1 && vec) {
+      // a few rows (the linearised entry's G): gemm_skinny.hpp, no 256-row tile
+      const dim3 g(gemm_skinny_grid(N));
+#define TVR_SK(F, MT)                                                                                  \
+  hipLaunchKernelGGL((gemm_skinny_kernel<F, MT>), g, dim3(SK_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
+                     ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_SK_F(F)                     \
+  switch ((M + 15) / 16) {              \
+    case 1: TVR_SK(F, 1); break;        \
+    case 2: TVR_SK(F, 2); break;        \
+    case 3: TVR_SK(F, 3); break;        \
+    default: TVR_SK(F, 4); break;       \
+  }
+      if (a_fmt == ACT_X2F16) { TVR_SK_F(ACT_X2F16); } else { TVR_SK_F(ACT_BF16); }
+#undef TVR_SK_F
+#undef TVR_SK
     } else {
-      launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, 0, vec, st);
+      PpPlan plan;
+      if (m && vec && epi != EPI_STATS) plan = plan_pp(M, N, K, a_fmt);
+      if (plan.ksplit > 1) {
+        TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, gemm_pingpong_grid(M, N),
+                                 plan.ksplit, m, st));
+      } else if (plan.tail_base > 0) {
+        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, true, st);
+        TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
+                                 gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st));
+      } else {
+        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, 0, vec, st);
+      }
     }
   } else {
     const float* Af = static_cast<const float*>(A);
@@ -1720,6 +1739,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     eg.out0 = (float*)(base + o_g);
     eg.ld0 = D1;
     eg.a_rows = (const int32_t*)(base + o_lin_vids) + lin_vid_off[l];
+    eg.skinny = 1;
     int rc = launch_gemm(EPI_BIAS, vact, d, fmt, m->w1[l], d, lin_nv[l], D1, d, eg, st, m);
     m->prof = prof;
     TVR_TRY(rc);

@@ -99,55 +99,54 @@ struct GemmEpi {
   float* raw;
   int raw_rows;
   int ld_raw;
+  // EPI_BIAS planar launches of at most SK_MAX_M rows that opt in run
+  // gemm_skinny.hpp (the linearised entry's G); the unembed keeps the pingpong
+  // kernel so its logits path and fused statistics share one GEMM
+  int skinny;
 };
 
 // torch.nn.functional.gelu (approximate='none'), TransformerLens act_fn "gelu":
-// x Phi(x), Phi from erfc(|x| / sqrt 2) = t exp(-z^2 + P(t)), t = 1 / (1 + z/2),
-// P the degree-9 Chebyshev fit of Press et al. (Numerical Recipes, erfcc;
-// relative error < 1.2e-7 on erfc everywhere).  Branch-free (the GEMM
-// epilogue applies it to every lane: ocml erff diverges into two paths, 3x the
-// instructions); |error| <= 1.2e-7 max(1, |x|), as 0.5 x (1 + erff(x / sqrt 2))
-// in fp32, and relative accuracy holds on the negative tail (no 1 + erf
-// cancellation).
+// x Phi(x) = max(x, 0) - |x| h,  h = erfc(|x| / sqrt 2) / 2,  with
+// erfc(z) = t (a1 + a2 t + ... + a5 t^4) exp(-z^2),  t = 1 / (1 + p z)
+// (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 on erfc), the 1/2 folded into
+// the exponent: h = t P(t) exp2(-x^2 log2(e) / 2 - 1).  One reciprocal, one
+// exp2, five polynomial steps, no branch or select (the GEMM epilogue applies
+// it to every lane and is VALU-bound on it: it replaced Press's degree-9 erfcc
+// form, 9 steps and a select).  |error| <= 1.7e-7 max(1, |x|) in fp32 against
+// the exact GELU (numpy fp32 emulation over |x| <= 12; the Press form: 1.4e-7).
+constexpr float GELU_P = 0.3275911f * 0.70710678118654752440f;  // p / sqrt 2 (t from |x|)
+constexpr float GELU_Q = -0.5f * 1.44269504088896341f;          // -log2(e) / 2
+constexpr float GELU_A1 = 0.254829592f, GELU_A2 = -0.284496736f, GELU_A3 = 1.421413741f,
+                GELU_A4 = -1.453152027f, GELU_A5 = 1.061405429f;
 __device__ __forceinline__ float gelu_erf(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float h = 0.5f * t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.44269504088896341f);  // erfc(z) / 2
-  return x * (x >= 0.0f ? 1.0f - h : h);
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(ax, GELU_P, 1.0f));
+  float p = GELU_A5;
+  p = fmaf(p, t, GELU_A4);
+  p = fmaf(p, t, GELU_A3);
+  p = fmaf(p, t, GELU_A2);
+  p = fmaf(p, t, GELU_A1);
+  p *= t;
+  const float h = p * __builtin_amdgcn_exp2f(fmaf(ax, ax * GELU_Q, -1.0f));
+  return fmaf(-ax, h, fmaxf(x, 0.0f));
 }
 
 // gelu_erf on two values with packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32:
 // the polynomial at half the VALU issue cycles); identical arithmetic.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
-  const f32x2 z = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752440f;
-  const f32x2 d = __builtin_elementwise_fma(z, f32x2{0.5f, 0.5f}, f32x2{1.0f, 1.0f});
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = __builtin_elementwise_fma(ax, f32x2{GELU_P, GELU_P}, f32x2{1.0f, 1.0f});
   const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2 p = {0.17087277f, 0.17087277f};
-#define TVR_G2(c) p = __builtin_elementwise_fma(p, t, f32x2{c, c})
-  TVR_G2(-0.82215223f);
-  TVR_G2(1.48851587f);
-  TVR_G2(-1.13520398f);
-  TVR_G2(0.27886807f);
-  TVR_G2(-0.18628806f);
-  TVR_G2(0.09678418f);
-  TVR_G2(0.37409196f);
-  TVR_G2(1.00002368f);
-  TVR_G2(-1.26551223f);
-#undef TVR_G2
-  const f32x2 a = __builtin_elementwise_fma(-z, z, p) * 1.44269504088896341f;
-  const f32x2 h = 0.5f * t * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-  return x * f32x2{x.x >= 0.0f ? 1.0f - h.x : h.x, x.y >= 0.0f ? 1.0f - h.y : h.y};
+  f32x2 p = {GELU_A5, GELU_A5};
+  p = __builtin_elementwise_fma(p, t, f32x2{GELU_A4, GELU_A4});
+  p = __builtin_elementwise_fma(p, t, f32x2{GELU_A3, GELU_A3});
+  p = __builtin_elementwise_fma(p, t, f32x2{GELU_A2, GELU_A2});
+  p = __builtin_elementwise_fma(p, t, f32x2{GELU_A1, GELU_A1});
+  p *= t;
+  const f32x2 e = __builtin_elementwise_fma(ax, ax * GELU_Q, f32x2{-1.0f, -1.0f});
+  const f32x2 h = p * f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  return __builtin_elementwise_fma(-ax, h, f32x2{fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)});
 }
 
 // One output element of the fused epilogues (v = acc + bias already); FMT is
