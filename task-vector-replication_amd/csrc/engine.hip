@@ -444,8 +444,8 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   if (planar) {
     const uint16_t* Ah = static_cast<const uint16_t*>(A);
     const bool vec = planar_epilogue_vec(epi, ep, N);
-    if (ep.skinny && epi == EPI_BIAS && M <= SK_MAX_M && !ep.out_rows && ep.k_split <= 1 && vec) {
-      // a few rows (the linearised entry's G): gemm_skinny.hpp, no 256-row tile
+    if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec) {
+      // a few rows (the linearised entry's G on a rank of a head split): gemm_skinny.hpp
       const dim3 g(gemm_skinny_grid(N));
 #define TVR_SK(F, MT)                                                                                  \
   hipLaunchKernelGGL((gemm_skinny_kernel<F, MT>), g, dim3(SK_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \

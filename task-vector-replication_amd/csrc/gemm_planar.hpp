@@ -107,30 +107,61 @@ __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n
 // wholly in range or out.  Without it, element-wise stores (one path per
 // instantiation: both in one body exceed the unroller's budget and the
 // accumulators go to scratch).
+// Every global load (the gathered output rows, the bias, the residual) is
+// issued ahead of the stores it feeds: s_waitcnt vmcnt counts loads and
+// stores together in issue order, so a load between two stores makes the
+// second wait for the first to reach memory.  The lane's output rows and
+// column biases are loaded once; the residual of row tile i + 1 is loaded
+// before row tile i is stored.
 template <int EPI, int FMT, bool VEC, int TM, int TN>
 __device__ __forceinline__ void gemm_epilogue16t(const GemmEpi& ep, const f32x4 (&acc)[TM][TN], int M, int N,
                                                  int row_base, int col_base, int lane) {
+  int orow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = min(row_base + i * 16 + (lane & 15), M - 1);
+    orow[i] = ep.out_rows ? ep.out_rows[m] : m;
+  }
+  f32x4 b4[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n0 = col_base + j * 16 + 4 * (lane >> 4);
-    if (n0 >= N) continue;
-    f32x4 b4 = {0.f, 0.f, 0.f, 0.f};
+    b4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (ep.bias) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) b4[r] = n0 + r < N ? ep.bias[n0 + r] : 0.f;
+      for (int r = 0; r < 4; ++r) b4[j][r] = n0 + r < N ? ep.bias[n0 + r] : 0.f;
     }
+  }
+  f32x4 rr[2][TN];
+  auto load_resid = [&](int i, f32x4 (&q)[TN]) {
+    if constexpr (EPI == EPI_RESID && VEC) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = row_base + i * 16 + (lane & 15);
-      if (m >= M) continue;
-      const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
-      const f32x4 v = acc[i][j] + b4;
+      for (int j = 0; j < TN; ++j) {
+        const int n0 = min(col_base + j * 16 + 4 * (lane >> 4), N - 4);
+        q[j] = *(const f32x4*)(ep.resid + (size_t)orow[i] * ep.ldr + n0);
+      }
+    }
+  };
+  load_resid(0, rr[0]);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if (i + 1 < TM) load_resid(i + 1, rr[(i + 1) & 1]);
+    const int m = row_base + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n0 = col_base + j * 16 + 4 * (lane >> 4);
+      if (n0 >= N) continue;
+      const f32x4 v = acc[i][j] + b4[j];
       if constexpr (VEC) {
-        epi_store4<EPI, FMT>(ep, orow, n0, v);
+        if constexpr (EPI == EPI_RESID)
+          st16<false>(ep.out0 + (size_t)orow[i] * ep.ld0 + n0, v + rr[i & 1][j]);
+        else
+          epi_store4<EPI, FMT>(ep, orow[i], n0, v);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (n0 + r < N) epi_store<EPI, FMT>(ep, orow, n0 + r, v[r]);
+          if (n0 + r < N) epi_store<EPI, FMT>(ep, orow[i], n0 + r, v[r]);
       }
     }
   }

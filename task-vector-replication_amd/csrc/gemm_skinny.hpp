@@ -9,11 +9,11 @@
 // the MFMA work) and 70 column tiles need a split-K partial round trip; such a
 // launch is a weight stream (N K 4 B: 183 MB per 2.8B layer), so this kernel
 // reads every weight element once, straight into registers, and spends its
-// MFMAs on 16-row tiles of the real rows only.  Measured at C3 (G of 32
-// vectors, N 17920, K 2560): about the split-K pingpong launch's ~65 us at 32
-// rows, 20 us less at 4 rows (rank 0 of an 8-way head split); a variant
-// reading 64 B per lane and plane per 4 k-steps without the register double
-// buffer ran 95 us (profiles/r02o/skinny_ab.txt).
+// MFMAs on 16-row tiles of the real rows only.  It streams W at ~2.5 TB/s
+// (16 rows x 64 B per load instruction), so it wins only where the 256-row
+// tile wastes the most: see SK_USE_M.  A variant reading 64 B per lane and
+// plane per 4 k-steps without the register double buffer ran slower still
+// (profiles/r02o/skinny_ab.txt).
 // Block = 4 waves over 32 output columns; wave w takes k-steps [w S / 4,
 // (w + 1) S / 4) of the S = K / 32 and all M rows: per k-step 2 W fragments
 // and MT A fragments (16 B per lane per plane, global -> VGPR, the next
@@ -34,6 +34,11 @@ constexpr int SK_THREADS = 256;  // 4 waves
 constexpr int SK_NT = 2;         // 16-column tiles per block (every wave computes all of them)
 constexpr int SK_COLS = 16 * SK_NT;
 constexpr int SK_MAX_M = 64;
+// The engine's policy (launch_gemm, ep.skinny launches): this kernel at most
+// 16 rows, the split-K pingpong launch above.  C3 rocprof (tag r02p): 72 us
+// at 32 rows against 59 us for the pingpong G; rank 0 of an 8-way head split
+// (4 rows): ~55 us against ~75 us.
+constexpr int SK_USE_M = 16;
 
 inline int gemm_skinny_grid(int N) { return (N + SK_COLS - 1) / SK_COLS; }
 
