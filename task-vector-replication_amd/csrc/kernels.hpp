@@ -181,9 +181,14 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
       __syncthreads();
       if (!col) continue;
       for (int p0 = 0; p0 < sn; p0 += ENTRY_POS_CHUNK) {
-        float acc[ENTRY_POS_CHUNK];
+        // the clean rows' values first: no load between this chunk's stores (s_waitcnt
+        // vmcnt counts loads and stores together, so a load after a store waits for it)
+        float sv[ENTRY_POS_CHUNK], acc[ENTRY_POS_CHUNK];
 #pragma unroll
-        for (int u = 0; u < ENTRY_POS_CHUNK; ++u) acc[u] = 0.f;
+        for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
+          acc[u] = 0.f;
+          sv[u] = snap[(size_t)(e.src_row + e.p0 + s0 + min(p0 + u, sn - 1)) * d + c];
+        }
         for (int k0 = 0; k0 < dh; k0 += ENTRY_K_CHUNK) {
           float wk[ENTRY_K_CHUNK];
 #pragma unroll
@@ -203,8 +208,7 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
 #pragma unroll
         for (int u = 0; u < ENTRY_POS_CHUNK; ++u) {
           if (p0 + u < sn) {
-            const int i = s0 + p0 + u, pos = e.p0 + i;
-            resid[(size_t)(e.row0 + i) * d + c] = snap[(size_t)(e.src_row + pos) * d + c] + (vc - acc[u]);
+            resid[(size_t)(e.row0 + s0 + p0 + u) * d + c] = sv[u] + (vc - acc[u]);
           }
         }
       }
@@ -212,18 +216,21 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
     return;
   }
   if (c >= d) return;
-  if (e.kind == 2) {  // TVR_SITE_ADD_ATTN_OUT_LASTPOS
-    for (int i = 0; i < e.n; ++i) {
-      const int pos = e.p0 + i;
-      resid[(size_t)(e.row0 + i) * d + c] =
-          snap[(size_t)(e.src_row + pos) * d + c] + vectors[(size_t)e.vec * d + c];
-    }
-  } else {  // NONE / SET_RESID_PRE_POS: copy rows, one of them from another run
-    for (int i = 0; i < e.n; ++i) {
-      const int pos = e.p0 + i;
+  // rows in batches of 8 whose loads precede their stores (as above)
+  const float add = e.kind == 2 ? vectors[(size_t)e.vec * d + c] : 0.f;  // TVR_SITE_ADD_ATTN_OUT_LASTPOS
+  constexpr int B = 8;
+  for (int i0 = 0; i0 < e.n; i0 += B) {
+    float v[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int pos = e.p0 + min(i0 + u, e.n - 1);
+      // NONE / SET_RESID_PRE_POS copy rows, one of them from another run
       const int srow = (e.kind == 3 && pos == e.patch_pos) ? e.src2_row : e.src_row + pos;
-      resid[(size_t)(e.row0 + i) * d + c] = snap[(size_t)srow * d + c];
+      v[u] = snap[(size_t)srow * d + c];
     }
+#pragma unroll
+    for (int u = 0; u < B; ++u)
+      if (i0 + u < e.n) resid[(size_t)(e.row0 + i0 + u) * d + c] = v[u] + add;
   }
 }
 

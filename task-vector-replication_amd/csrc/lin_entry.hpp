@@ -213,25 +213,39 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
   }
   __syncthreads();
   // combine + store: thread t takes columns col0 + 4 (t & 63) .. +3 of rows t >> 6, + 4, ...
+  // in batches of 8 rows whose y_c / G loads are all issued before the batch's
+  // stores (qkv is read at clean rows and written at entering rows, so the
+  // compiler may not move a load past a store; one load after a store would
+  // make it wait for that store to reach memory: s_waitcnt vmcnt counts both).
   const int cl = 4 * (threadIdx.x & 63), n0 = col0 + cl, n3 = 3 * d;
   if (n0 >= N) return;
   const f32x4 b = *(const f32x4*)(b1 + n0), c = *(const f32x4*)(c1 + n0);
-#pragma unroll 4
-  for (int r = threadIdx.x >> 6; r < mb.rows; r += LIN_THREADS / 64) {
-    const int4 q = rrow[r];
-    const f32x4 k = rcoef[r];
-    const f32x4 v = *(const f32x4*)(tile + r * LIN_LDR + cl);
-    const f32x4 yc = n0 < n3 ? *(const f32x4*)(qkv + (size_t)q.y * n3 + n0)
-                             : *(const f32x4*)(raw_h + (size_t)q.y * d_mlp + (n0 - n3));
-    const f32x4 gv = *(const f32x4*)(G + (size_t)q.z * N + n0);
-    f32x4 y;
+  constexpr int RB = 8, RS = LIN_THREADS / 64;
+  for (int r0 = threadIdx.x >> 6; r0 < mb.rows; r0 += RS * RB) {
+    int4 q[RB];
+    f32x4 yc[RB], gv[RB];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = k[0] * (yc[e] - b[e]) + k[1] * c[e] + k[2] * (gv[e] - v[e]) + b[e];
-    if (n0 < n3) {
-      *(f32x4*)(qkv + (size_t)q.x * n3 + n0) = y;
-    } else {
-      const f32x2 g01 = gelu_erf2(f32x2{y[0], y[1]}), g23 = gelu_erf2(f32x2{y[2], y[3]});
-      store_act4<FMT>(out1h + (size_t)q.x * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
+    for (int i = 0; i < RB; ++i) {
+      q[i] = rrow[min(r0 + RS * i, mb.rows - 1)];
+      yc[i] = n0 < n3 ? *(const f32x4*)(qkv + (size_t)q[i].y * n3 + n0)
+                      : *(const f32x4*)(raw_h + (size_t)q[i].y * d_mlp + (n0 - n3));
+      gv[i] = *(const f32x4*)(G + (size_t)q[i].z * N + n0);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = r0 + RS * i;
+      if (r >= mb.rows) break;
+      const f32x4 k = rcoef[r];
+      const f32x4 v = *(const f32x4*)(tile + r * LIN_LDR + cl);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = k[0] * (yc[i][e] - b[e]) + k[1] * c[e] + k[2] * (gv[i][e] - v[e]) + b[e];
+      if (n0 < n3) {
+        *(f32x4*)(qkv + (size_t)q[i].x * n3 + n0) = y;
+      } else {
+        const f32x2 g01 = gelu_erf2(f32x2{y[0], y[1]}), g23 = gelu_erf2(f32x2{y[2], y[3]});
+        store_act4<FMT>(out1h + (size_t)q[i].x * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
+      }
     }
   }
 }
