@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gemm_planar.hpp"
 
 namespace tvr {
@@ -344,23 +346,33 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
   frag fa[4][2], fwl[2][2], fwh[2][2];
 
-  auto read_a = [&](const uint16_t* base, int i0) {
+  // 16-row slices of this wave's 128 rows that hold real rows (A rows past M
+  // are staged as copies of row M - 1).  A wave with fewer than 8 runs the
+  // K loop's PART copy, which skips the fragment reads and MFMAs of the padding
+  // slices (the staging and the barriers stay: the other group needs them):
+  // the last m-block of every launch, and most blocks of the small-M layer
+  // sweeps (C2: M = 156 + 52 l rows in 256-row tiles).
+  const int vi = __builtin_amdgcn_readfirstlane(min(8, max(0, (M - m0 - wr * 128 + 15) >> 4)));  // wave-uniform
+  auto read_a = [&](const uint16_t* base, int i0, auto part) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+      if (!decltype(part)::value || i0 + i < vi)
 #pragma unroll
-      for (int f = 0; f < 2; ++f) fa[i][f] = *(const frag*)(base + aoff[f] + (i0 + i) * 16 * BK);
+        for (int f = 0; f < 2; ++f) fa[i][f] = *(const frag*)(base + aoff[f] + (i0 + i) * 16 * BK);
   };
-  auto read_w = [&](const uint16_t* base, int j0, frag (&fw)[2][2]) {
+  auto read_w = [&](const uint16_t* base, int j0, frag (&fw)[2][2], auto part) {
+    if (decltype(part)::value && vi == 0) return;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
   };
-  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], int ib = 0, int ie = 4) {
+  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part) {
 #pragma unroll
-    for (int i = ib; i < ie; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
+        if (decltype(part)::value && i0 + i >= vi) continue;
         f32x4 c = acc[i0 + i][j0 + j];
         if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
@@ -402,28 +414,34 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
 
   unsigned long long d_loop0 = 0, d_loop1 = 0;
   if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
-  for (int kt = 0; kt < nk; ++kt) {
-    const uint16_t* cur = lds + (kt & 1) * BUF;
-    // q1: Q(A_lo, W_lo)
-    read_a(cur, 0);
-    read_w(cur, 0, fwl);
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
-    stage(1, kt + 1);
-    TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl));
-    // q2: Q(A_lo, W_hi)
-    read_w(cur, 2, fwh);
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
-    stage(3, kt + 1);
-    TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh));
-    // q3: Q(A_hi, W_hi)
-    read_a(cur, 4);
-    stage(0, kt + 2);
-    TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh));
-    // q4: Q(A_hi, W_lo)
-    if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
-    stage(2, kt + 2);
-    TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl));
-  }
+  auto kloop = [&](auto part) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint16_t* cur = lds + (kt & 1) * BUF;
+      // q1: Q(A_lo, W_lo)
+      read_a(cur, 0, part);
+      read_w(cur, 0, fwl, part);
+      if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
+      stage(1, kt + 1);
+      TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part));
+      // q2: Q(A_lo, W_hi)
+      read_w(cur, 2, fwh, part);
+      if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+      stage(3, kt + 1);
+      TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part));
+      // q3: Q(A_hi, W_hi)
+      read_a(cur, 4, part);
+      stage(0, kt + 2);
+      TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part));
+      // q4: Q(A_hi, W_lo)
+      if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
+      stage(2, kt + 2);
+      TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part));
+    }
+  };
+  if (vi == 8)
+    kloop(std::integral_constant<bool, false>{});
+  else
+    kloop(std::integral_constant<bool, true>{});
 #undef TVR_PP_CLUSTER
   if constexpr (VAR == 6 || VAR == 8) d_loop1 = __builtin_amdgcn_s_memtime();
   if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset
