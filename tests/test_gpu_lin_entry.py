@@ -24,6 +24,7 @@ import torch
 import tvr_amd
 from conftest import TINY_STD, make_oracle
 from oracle import reference_experiments as R
+from tvr_amd import experiments as E
 
 pytestmark = pytest.mark.gpu
 
@@ -193,3 +194,35 @@ def test_lin_entry_at_headline_widths(name, gemm, kshot, monkeypatch):
     else:
         assert (cies["1"] - cies["0"]).abs().max().item() <= 5e-2 * pmax
     model._check_range("lin entry headline widths")
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,gemm,kshot", [("pythia-2.8b", "x2f16", 4), ("pythia-6.9b", "bf16", 5)],
+                         ids=["pythia-2.8b-x2f16", "pythia-6.9b-bf16"])
+def test_lin_entry_head_shard_at_headline_widths(name, gemm, kshot, monkeypatch):
+    """One rank's share of an 8-way head split (heads h = 0 mod 8): 4 distinct
+    vectors per entry layer, so the linearised entry's G = v W1^T runs on
+    gemm_skinny_kernel (<= 16 rows) at the real K / N (2560 / 17920, 4096 /
+    28672), against the full entry GEMM at the bars of the test above."""
+    cfg = tvr_amd.get_config(name).with_(n_layers=3)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok, gemm=gemm)
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 2, kshot, seed=1234)
+    answers = [int(t) for t in model.forward_clean(prompts, topk=1)["topk"][:, 0].tolist()]
+    pmax = model.forward_clean(prompts, targets=answers)["prob"].max().item()
+    g = torch.Generator().manual_seed(5)
+    mean = (torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5).cuda()
+    heads = list(range(0, cfg.n_heads, 8))
+    sums = {}
+    for lin in ("1", "0"):
+        monkeypatch.setenv("TVR_LIN_ENTRY", lin)
+        sums[lin] = E.causal_indirect_effect_sums(mean, prompts, answers, model, heads=heads).cpu().double()
+    big = sums["0"].abs().max().item()
+    assert big > 1e-3
+    other = [h for h in range(cfg.n_heads) if h not in heads]
+    assert sums["1"][:, other].abs().max().item() == 0.0
+    bar = 1e-4 * big + 1e-7 if gemm == "x2f16" else 5e-2 * pmax
+    assert (sums["1"] - sums["0"]).abs().max().item() <= bar
+    model._check_range("lin entry head shard")
