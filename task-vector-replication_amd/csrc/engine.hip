@@ -31,6 +31,7 @@
 #include "gemm_x3bf16.hpp"
 #include "kernels.hpp"
 #include "lin_entry.hpp"
+#include "entry_mfma.hpp"
 
 using namespace tvr;
 
@@ -1544,6 +1545,29 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     e.vec = s.vec;
     ents[k] = e;
   }
+  // entry layers' head-replacement sites grouped by head, at most ENTRY_GROUP per
+  // group (entry_mfma.hpp); ent_other: the layer has sites of other kinds (entry_kernel)
+  std::vector<char> ent_other(L + 1, 0);
+  std::vector<int32_t> egidx;
+  std::vector<int2> egroups;
+  std::vector<int> eg_beg(L + 1, 0), eg_cnt(L + 1, 0);
+  for (int l = 0; l <= L; ++l) {
+    eg_beg[l] = (int)egroups.size();
+    std::map<int, std::vector<int>> byhead;
+    for (int k = l > 0 ? cnt_le[l - 1] : 0; k < cnt_le[l]; ++k) {
+      if (ents[k].kind == TVR_SITE_REPLACE_HEAD_ALLPOS)
+        byhead[ents[k].head].push_back(k);
+      else
+        ent_other[l] = 1;
+    }
+    for (const auto& hv : byhead)
+      for (size_t a = 0; a < hv.second.size(); a += ENTRY_GROUP) {
+        const size_t b = std::min(hv.second.size(), a + (size_t)ENTRY_GROUP);
+        egroups.push_back(make_int2((int)egidx.size(), (int)(b - a)));
+        egidx.insert(egidx.end(), hv.second.begin() + a, hv.second.begin() + b);
+      }
+    eg_cnt[l] = (int)egroups.size() - eg_beg[l];
+  }
   // algorithmic bytes of each layer's entry launch (profiling): the clean rows
   // read and the patched rows written, the vector, and for REPLACE_HEAD the
   // head's z rows plus its W_O slice once per distinct head
@@ -1643,6 +1667,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const size_t o_lin_rows = cv.take<LinRow>(lin_rows.size());
   const size_t o_lin_mbs = cv.take<LinMB>(lin_mbs.size());
   const size_t o_lin_vids = cv.take<int32_t>(lin_vids.size());
+  const size_t o_egidx = cv.take<int32_t>(egidx.size());
+  const size_t o_egroups = cv.take<int2>(egroups.size());
   const size_t o_resid = cv.take<float>((size_t)RA * d);
   const size_t o_xn = cv.take<float>((size_t)RA * d);
   const size_t o_qkv = cv.take<float>((size_t)RA * 3 * d);
@@ -1673,6 +1699,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     ub.add(o_lin_mbs, lin_mbs);
     ub.add(o_lin_vids, lin_vids);
   }
+  ub.add(o_egidx, egidx);
+  ub.add(o_egroups, egroups);
   TVR_TRY(flush_uploads(m, st, base, ub));
 
   const int fmt = act_fmt(m);
@@ -1695,15 +1723,34 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     const float* snap = trace->resid + (size_t)l * tstride;
     const float* zsnap = l > 0 ? trace->z + (size_t)(l - 1) * tstride : nullptr;
     const float* w2 = l > 0 ? m->layers[l - 1].w2 : nullptr;
-    const size_t zbytes = (size_t)std::min(maxT, ENTRY_LDS_POS) * c.d_head * sizeof(float);
-    if (zbytes > 64 * 1024)
-      TVR_HIP(hipFuncSetAttribute((const void*)entry_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)zbytes));
+    const dim3 eg(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS);
     ProfSpan ps(m, st);
-    hipLaunchKernelGGL(entry_kernel, dim3(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS),
-                       dim3(ENTRY_THREADS), zbytes, st, d_ents + k0, snap, zsnap, w2, m->K2, vectors,
-                       a.resid, d, c.d_head);
-    TVR_HIP(hipGetLastError());
+    const bool mf = eg_cnt[l] > 0 && (c.d_head == 16 || c.d_head == 64 || c.d_head == 80 || c.d_head == 128);
+    if (mf) {
+      const dim3 gg(eg_cnt[l], (d + ENTRY_THREADS - 1) / ENTRY_THREADS);
+      const int32_t* gidx = (const int32_t*)(base + o_egidx);
+      const int2* grps = (const int2*)(base + o_egroups) + eg_beg[l];
+#define TVR_ENTRY_MF(DH)                                                                                   \
+  hipLaunchKernelGGL(entry_replace_mfma_kernel<DH>, gg, dim3(ENTRY_THREADS), 0, st, d_ents, gidx, grps, snap, \
+                     zsnap, w2, m->K2, vectors, a.resid, d)
+      switch (c.d_head) {
+        case 16: TVR_ENTRY_MF(16); break;
+        case 64: TVR_ENTRY_MF(64); break;
+        case 80: TVR_ENTRY_MF(80); break;
+        default: TVR_ENTRY_MF(128); break;
+      }
+#undef TVR_ENTRY_MF
+      TVR_HIP(hipGetLastError());
+    }
+    if (ent_other[l] || !mf) {
+      const size_t zbytes = mf ? 0 : (size_t)std::min(maxT, ENTRY_LDS_POS) * c.d_head * sizeof(float);
+      if (zbytes > 64 * 1024)
+        TVR_HIP(hipFuncSetAttribute((const void*)entry_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)zbytes));
+      hipLaunchKernelGGL(entry_kernel, eg, dim3(ENTRY_THREADS), zbytes, st, d_ents + k0, snap, zsnap, w2, m->K2,
+                         vectors, a.resid, d, c.d_head, mf ? 1 : 0);
+      TVR_HIP(hipGetLastError());
+    }
     ps.done(TVR_HBM_ENTRY, entry_bytes[l]);
     return TVR_OK;
   };

@@ -1,0 +1,110 @@
+// entry_mfma.hpp — the REPLACE_HEAD site entry on the fp32 matrix cores.
+//
+// A head-replacement site (layer e-1, head h, vector v) enters layer e with
+//     resid[i][c] = snap[p0 + i][c] + v[c] - sum_k z[p0 + i][h dh + k] W_O[c][h dh + k]
+// at every position i (kernels.hpp entry_kernel, parallel residual, SURVEY §7,
+// scratch2.py:188).  entry_kernel does the z . W_O product on the VALU (one
+// FMA per (position, column, k) and thread: 1.2 G FMAs per C3 entry layer);
+// here it is a [16 positions x dh] x [dh x 64 columns] tile per wave on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products, as the attention kernel).
+// Grid = (groups, ceil(d / 256)), 4 waves of 64 columns each; a group is up to
+// ENTRY_GROUP sites of one head (the host groups a layer's REPLACE_HEAD entries),
+// whose W_O[h] columns the wave reads once into registers: the launch was bound
+// by re-reading the 80 KB W_O slice of a 256-column block for every site.  The
+// MFMA's k index is a permutation applied to both operands: lane group g
+// supplies k = g CH + j at k-step j (CH = dh / 4), so a lane's B
+// operand is CH consecutive floats of one W_O row (float4 loads) and its A
+// operand CH consecutive floats of one z row, read from the z tile in LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gemm_f32.hpp"
+#include "kernels.hpp"
+
+namespace tvr {
+
+constexpr int ENTRY_GROUP = 4;  // sites of one head per block: W_O[h] read once for them
+
+template <int DH>
+__global__ void __launch_bounds__(ENTRY_THREADS)
+entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __restrict__ gidx,
+                          const int2* __restrict__ groups, const float* __restrict__ snap,
+                          const float* __restrict__ zsnap, const float* __restrict__ w2, int ldw2,
+                          const float* __restrict__ vectors, float* __restrict__ resid, int d) {
+  constexpr int CH = DH / 4;  // k values per lane group
+  static_assert(DH % 16 == 0, "d_head");
+  __shared__ __attribute__((aligned(16))) float zt[16 * (DH + 4)];  // 16 positions x DH (+4: conflict-free rows)
+  constexpr int LDZ = DH + 4;
+  const int2 grp = groups[blockIdx.x];  // entries gidx[grp.x .. + grp.y): REPLACE_HEAD sites of one head
+  const int head = ents[gidx[grp.x]].head;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * ENTRY_THREADS + wave * 64;  // this wave's first column
+
+  // B operands: W_O row (column c = n0 + 16 nt + li), k = g CH .. g CH + CH - 1
+  float wb[4][CH];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int c = min(n0 + 16 * nt + li, d - 1);
+    const float* wr = w2 + (size_t)c * ldw2 + head * DH + g * CH;
+#pragma unroll
+    for (int q = 0; q < CH; q += 4) {
+      const float4 v4 = *(const float4*)(wr + q);
+      wb[nt][q] = v4.x; wb[nt][q + 1] = v4.y; wb[nt][q + 2] = v4.z; wb[nt][q + 3] = v4.w;
+    }
+  }
+  for (int gi = 0; gi < grp.y; ++gi) {
+    const EntryDesc e = ents[gidx[grp.x + gi]];
+    for (int t0 = 0; t0 < e.n; t0 += 16) {
+      const int tn = min(16, e.n - t0);
+      __syncthreads();  // the previous tile's reads are done
+      for (int x = threadIdx.x; x < 16 * (DH / 4); x += ENTRY_THREADS) {
+        const int r = x / (DH / 4), q = (x - r * (DH / 4)) * 4;
+        const float4 v4 = *(const float4*)(zsnap + (size_t)(e.src_row + e.p0 + t0 + min(r, tn - 1)) * d +
+                                           e.head * DH + q);
+        *(float4*)(zt + r * LDZ + q) = v4;
+      }
+      __syncthreads();
+      if (n0 >= d) continue;  // (a wave past d joins the barriers only)
+      // the clean rows' values and the vector first (no load between the stores below)
+      f32x4 sv[4];
+      float vc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int c = min(n0 + 16 * nt + li, d - 1);
+        vc[nt] = vectors[(size_t)e.vec * d + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sv[nt][r] = snap[(size_t)(e.src_row + e.p0 + t0 + min(4 * g + r, tn - 1)) * d + c];
+      }
+      float za[CH];  // A operand: z row li, k = g CH ..
+#pragma unroll
+      for (int q = 0; q < CH; q += 4) {
+        const f32x4 v4 = *(const f32x4*)(zt + li * LDZ + g * CH + q);
+        za[q] = v4[0]; za[q + 1] = v4[1]; za[q + 2] = v4[2]; za[q + 3] = v4[3];
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};  // two chains (dependent-issue latency)
+#pragma unroll
+        for (int j = 0; j < CH; j += 2) {
+          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j], wb[nt][j], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j + 1], wb[nt][j + 1], a1, 0, 0, 0);
+        }
+        acc[nt] = a0 + a1;  // D[position 4 g + r][column li]
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int c = n0 + 16 * nt + li;
+        if (c >= d) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < tn) resid[(size_t)(e.row0 + t0 + 4 * g + r) * d + c] = sv[nt][r] + (vc[nt] - acc[nt][r]);
+      }
+    }
+  }
+}
+
+}  // namespace tvr

@@ -163,11 +163,12 @@ constexpr int ENTRY_LDS_POS = 128;
 __global__ void __launch_bounds__(ENTRY_THREADS)
 entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
              const float* __restrict__ zsnap, const float* __restrict__ w2, int ldw2,
-             const float* __restrict__ vectors, float* __restrict__ resid, int d, int dh) {
+             const float* __restrict__ vectors, float* __restrict__ resid, int d, int dh, int skip_replace) {
   extern __shared__ __attribute__((aligned(16))) float zs[];
   const EntryDesc e = ents[blockIdx.x];
   const int c = blockIdx.y * ENTRY_THREADS + threadIdx.x;
-  if (e.kind == 1) {  // TVR_SITE_REPLACE_HEAD_ALLPOS
+  if (e.kind == 1) {  // TVR_SITE_REPLACE_HEAD_ALLPOS (unless entry_mfma.hpp takes them)
+    if (skip_replace) return;
     const bool col = c < d;  // no early return: every thread joins the barriers
     const float* w = w2 + (size_t)(col ? c : 0) * ldw2 + e.head * dh;
     const float vc = col ? vectors[(size_t)e.vec * d + c] : 0.f;
