@@ -72,7 +72,7 @@ def gemm_variant(name):
 
 
 # the HBM-bound kernels (bench.py hbm_kernels names)
-HBM_KERNELS = {"lin_entry_kernel": "lin_entry", "entry_kernel": "entry", "lnpre_kernel": "lnpre", "attention_mfma_kernel": "attention",
+HBM_KERNELS = {"lin_entry_kernel": "lin_entry", "entry_replace_mfma_kernel": "entry", "entry_kernel": "entry", "lnpre_kernel": "lnpre", "attention_mfma_kernel": "attention",
                "stats_merge_kernel": "row_stats", "row_stats_kernel": "row_stats", "capture_partial_kernel": "capture",
                "capture_finish_kernel": "capture"}
 
