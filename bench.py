@@ -33,6 +33,15 @@ value = units of all ranks / max-rank time.  The timed region runs with no
 profiling; the kernel timings of ``roofline`` / ``hbm_kernels`` come from a
 separate profiled pass of the same step.
 
+``--gpus N`` without torchrun (no ``WORLD_SIZE`` in the environment): this
+process touches no GPU and starts N child ranks of itself (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT), each on GPU
+LOCAL_RANK, waits for them and exits with the worst exit status; rank 0 prints
+the JSON line, whose ``n_gpus`` is the world size the process group saw.
+``--dist-backend gloo`` rehearses several ranks on one GPU;
+``--launch-check`` runs only the rendezvous and the timing collectives (no
+GPU: the CPU test of the launcher).
+
 Extra JSON objects: ``roofline`` (dominant kernel = the GEMM family, achieved
 from HIP events on the engine's launch stream), ``cpu_baseline`` (the CPU
 oracle running the reference's loop structure on a bounded sample, rank 0 at
@@ -97,7 +106,61 @@ def parse():
     ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks on one GPU")
+    ap.add_argument("--launch-check", dest="launch_check", action="store_true",
+                    help="only the rank launch, rendezvous and max-over-ranks timing (no GPU work; CPU test)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` without torchrun: start N child ranks of this script and
+    wait for them.  Called before anything in this process touches the GPU
+    (children are fresh processes, never an exec of this one).  A rank that
+    fails ends the others (they would block in a collective) by their PIDs."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def launch_check(rank: int, world: int, backend: str) -> None:
+    """The launcher's CPU rehearsal: rendezvous, barrier, max-over-ranks time."""
+    dist.init_process_group(backend)
+    t0 = time.perf_counter()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    times = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(times, el)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "backend": backend,
+                          "rank_elapsed_s": [t.item() for t in times], "max_elapsed_s": el.item()}), flush=True)
+    dist.destroy_process_group()
 
 
 def pmc_summary(family, workload):
@@ -230,9 +293,14 @@ DTYPES = {"x2f16": "f32 (x2f16 emulation: fp32 operands as 2 fp16 planes, 3 MFMA
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.launch_check:
+        launch_check(rank, world, "gloo" if args.dist_backend == "nccl" else args.dist_backend)
+        return
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     if world > 1:
@@ -292,6 +360,8 @@ def main():
             dist.all_reduce(cie)
         return cie
 
+    rank_times = []
+
     def timed(warmup, steps, profile):
         for i in range(warmup):
             step()
@@ -309,12 +379,16 @@ def main():
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         if world > 1:
+            times = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(times, t)
+            rank_times[:] = [x.item() for x in times]
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item(), cie
 
     elapsed, cie = timed(args.warmup, args.steps, False)
+    rank_elapsed = list(rank_times)
     value = units_total * args.steps / elapsed
 
     # --- roofline of the dominant kernel + HBM-bound kernels: a separate profiled pass
@@ -360,7 +434,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "patched prompts/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
@@ -375,6 +449,8 @@ def main():
             "sites_per_step_per_gpu": units_rank,
             "parallelism": parallelism,
             "shard": shard,
+            "dist_backend": args.dist_backend if world > 1 else None,
+            "rank_elapsed_s": [round(x, 4) for x in rank_elapsed] if world > 1 else None,
         },
         "roofline": {
             "bound": "mfma",

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 8
+#define TVR_ABI_VERSION 9
 
 enum tvr_status {
   TVR_OK = 0,
@@ -156,7 +156,12 @@ int tvr_model_range_status(tvr_model* model, void* stream);
  * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */
 int tvr_trace_create(tvr_model* model, int32_t max_seqs, int32_t max_tokens,
                      tvr_trace** out);
+/* Destroying a trace with a deferred clean forward pending runs it first (on
+ * the null stream) so the caller's out_prob / out_topk are written. */
 int tvr_trace_destroy(tvr_trace* trace);
+/* Run a pending deferred clean forward now (tvr_forward_clean_deferred) on
+ * `stream`; no-op otherwise. */
+int tvr_trace_flush(tvr_trace* trace, void* stream);
 /* Copy a traced hook into a caller device buffer [n_tokens][d] (async on
  * `stream`): what = TVR_TRACE_RESID_PRE gives blocks.{layer}.hook_resid_pre
  * (layer == n_layers: the final residual), TVR_TRACE_Z blocks.{layer}.attn.hook_z. */

@@ -1,8 +1,11 @@
 """ctypes binding of ``libtvr.so`` (the C ABI declared in include/tvr.h).
 
 The reference is Python, so its binding to a native engine is a ctypes stub
-(INTEGRATION.md).  Loading fails loudly: there is no CPU fallback anywhere in
-the product path.
+(INTEGRATION.md).  The compute entry points (clean forward, patch sweep, head
+projection, logits) are called as torch.library operators ``torch.ops.tvr.*``
+registered by ``_tvr_ops.so`` (csrc/torch_ops.cpp, over the same C ABI:
+load_ops); handle lifetime, GEMM mode, traces and profiling stay on ctypes.
+Loading fails loudly: there is no CPU fallback anywhere in the product path.
 """
 from __future__ import annotations
 
@@ -11,6 +14,7 @@ import os
 from pathlib import Path
 
 LIB_NAME = "libtvr.so"
+OPS_NAME = "_tvr_ops.so"
 # TVR_LIB: another in-tree build of the engine (same-box A/B of two builds)
 LIB_PATH = Path(os.environ["TVR_LIB"]).resolve() if os.environ.get("TVR_LIB") else Path(__file__).resolve().parent / LIB_NAME
 
@@ -66,7 +70,7 @@ class CHbmStats(ctypes.Structure):
 HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats", "lin_entry")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 8  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 9  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
@@ -81,6 +85,7 @@ SIGNATURES = {
     "tvr_trace_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "tvr_trace_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "tvr_trace_flush": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tvr_trace_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, c_f32p,
                                       ctypes.c_void_p]),
     "tvr_trace_num_tokens": (ctypes.c_int32, [ctypes.c_void_p]),
@@ -125,7 +130,12 @@ SIGNATURES = {
     "tvr_profile_read_hbm": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CHbmStats)]),
 }
 
+OPS_PATH = LIB_PATH.parent / OPS_NAME
+# the torch.library operators _tvr_ops.so registers (csrc/torch_ops.cpp)
+OPS = ("forward_clean", "patch_sweep", "project_heads", "forward_logits")
+
 _LIB = None
+_OPS_LOADED = False
 
 
 class EngineError(RuntimeError):
@@ -152,6 +162,21 @@ def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     if path is None:
         _LIB = lib
     return lib
+
+
+def load_ops():
+    """Register the ``torch.ops.tvr`` operators (once; after libtvr.so, which
+    they link from their own directory).  Raises if the extension is missing."""
+    global _OPS_LOADED
+    import torch
+    load()
+    if not _OPS_LOADED:
+        if not OPS_PATH.exists():
+            raise EngineError(f"{OPS_PATH} not found: the torch operator extension is not built (no CPU fallback "
+                              "exists); run `make -C task-vector-replication_amd/csrc`")
+        torch.ops.load_library(str(OPS_PATH))
+        _OPS_LOADED = True
+    return torch.ops.tvr
 
 
 def check(rc: int, what: str) -> None:

@@ -114,6 +114,9 @@ struct tvr_model {
   uint16_t* planes = nullptr;
   unsigned* range_flag = nullptr;  // device word: X2F16 input out of range since the last status read
   std::vector<MatW> w1, w2;
+  // TVR_GEMM_BF16 only: W1's Q / K rows [0, 2d) as one fp16 plane of
+  // wscale * W (the attention-score projections run on fp16 operands: launch_w1)
+  std::vector<MatW> w1qk;
   MatW wu;
   char* ws = nullptr;
   size_t ws_bytes = 0;
@@ -319,6 +322,10 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
   if (vec) { TVR_PP1(E, F, true); } else { TVR_PP1(E, F, false); }
 #define TVR_PP1F(E) \
   if (a_fmt == ACT_X2F16) { TVR_PP1V(E, ACT_X2F16); } else { TVR_PP1V(E, ACT_BF16); }
+  if (a_fmt == ACT_F16) {  // the bf16 mode's Q / K columns: plain fp32 outputs only (launch_gemm checks)
+    TVR_PP1V(EPI_BIAS, ACT_F16);
+    return;
+  }
   switch (epi) {
     case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
     case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
@@ -353,6 +360,9 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
   if (a_fmt == ACT_X2F16)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_F16)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
@@ -383,7 +393,7 @@ struct PpPlan {
 };
 PpPlan plan_pp(int M, int N, int K, int a_fmt) {
   PpPlan p;
-  const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_BF16 ? 64 : 32);
+  const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_X2F16 ? 32 : 64);
   if (tiles < 192) {
     p.ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
     return p;
@@ -431,8 +441,10 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   if (epi == EPI_STATS && (!planar || N % 4 != 0 || !ep.stats))
     return fail(TVR_ERR_INVALID, "gemm: the fused statistics epilogue needs a planar format, N % 4 == 0 and a "
                                  "statistics buffer");
+  if (a_fmt == ACT_F16 && epi != EPI_BIAS)
+    return fail(TVR_ERR_INVALID, "gemm: the fp16 operand format has the plain (bias) epilogue only");
   if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0) ||
-      (a_fmt == ACT_BF16 && K % 64 != 0))
+      ((a_fmt == ACT_BF16 || a_fmt == ACT_F16) && K % 64 != 0))
     return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes, K of 64 for "
                                      "bf16; K=" + std::to_string(K) + ")");
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -441,11 +453,13 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     ev1 = prof_event(m);
     if (ev0) TVR_HIP(hipEventRecord(ev0, st));
   }
-  const float acc_scale = (a_fmt == ACT_BF16) ? 1.0f : 1.0f / (W.wscale * X2_ASCALE);
+  // X2F16: both operands scaled (W by wscale, A by 16); F16: W only; BF16: neither
+  const float acc_scale = a_fmt == ACT_BF16 ? 1.0f : a_fmt == ACT_F16 ? 1.0f / W.wscale : 1.0f / (W.wscale * X2_ASCALE);
   if (planar) {
     const uint16_t* Ah = static_cast<const uint16_t*>(A);
     const bool vec = planar_epilogue_vec(epi, ep, N);
-    if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec) {
+    if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec &&
+        a_fmt != ACT_F16) {
       // a few rows (the linearised entry's G on a rank of a head split): gemm_skinny.hpp
       const dim3 g(gemm_skinny_grid(N));
 #define TVR_SK(F, MT)                                                                                  \
@@ -512,8 +526,8 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     // minimal operand bytes: W read once (fp32 4, 3 bf16 planes 6, 2 fp16 planes 4, bf16 2 B per element),
     // A once in its format (fp32 / x2f16 4, bf16 2), C once as fp32
     // (EPI_STATS: the per-tile statistics records instead of C)
-    const double wbytes = W.x ? 6.0 : (a_fmt == ACT_BF16 ? 2.0 : 4.0);
-    const double abytes = a_fmt == ACT_BF16 ? 2.0 : 4.0;
+    const double wbytes = W.x ? 6.0 : (a_fmt == ACT_BF16 || a_fmt == ACT_F16 ? 2.0 : 4.0);
+    const double abytes = a_fmt == ACT_BF16 || a_fmt == ACT_F16 ? 2.0 : 4.0;
     const double cbytes = epi == EPI_STATS ? 4.0 * M * (double)ep.stats_tiles * (2 + 2 * ep.stats_k)
                                            : 4.0 * M * (double)N;
     const int kind = epi == EPI_SPLIT_GELU_ACT ? (int)EPI_SPLIT_GELU : epi == EPI_STATS ? (int)EPI_BIAS : epi;
@@ -629,8 +643,8 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   else
     hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
   TVR_HIP(hipGetLastError());
-  // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B, bf16 2 B per element)
-  ps.done(TVR_HBM_LNPRE, (double)rows * d * (4.0 + (fmt == ACT_BF16 ? 2.0 : 4.0)));
+  // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element)
+  ps.done(TVR_HBM_LNPRE, (double)rows * d * 8.0);
   return TVR_OK;
 }
 
@@ -721,6 +735,36 @@ double attention_bytes(int d, int q_rows, int kv_rows, int fmt, int zf_rows) {
          (double)zf_rows * d * 4.0;
 }
 
+// W1 GEMM over LayerNorm outputs xn (a.fmt), columns [c0, c0 + N) of W1, with
+// an epilogue ep already addressed to column c0 (EPI_SPLIT_GELU_ACT planar /
+// EPI_SPLIT_GELU fp32).  TVR_GEMM_BF16 runs the attention-score columns
+// (Q, K: [0, 2d)) on the fp16 operands instead (W1's fp16 Q / K plane, xn's
+// fp16 plane 1: store_ln4) with plain fp32 stores, the rest on bf16.
+int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const GemmEpi& ep, hipStream_t st) {
+  const int d = m->cfg.d_model;
+  const int fmt = act_fmt(m);
+  const int epi = fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU;
+  const int nqk = fmt == ACT_BF16 && !m->w1qk.empty() ? std::min(std::max(2 * d - c0, 0), N) : 0;
+  if (nqk > 0) {
+    GemmEpi e{};
+    e.bias = ep.bias;
+    e.out0 = ep.out0;
+    e.ld0 = ep.ld0;
+    e.a_rows = ep.a_rows;
+    e.out_rows = ep.out_rows;
+    TVR_TRY(launch_gemm(EPI_BIAS, static_cast<const uint16_t*>(xn) + d, d, ACT_F16,
+                        m->w1qk[l].rows((size_t)c0 * d), d, M, nqk, d, e, st, m));
+    if (nqk == N) return TVR_OK;
+  }
+  GemmEpi e = ep;
+  if (nqk > 0) {
+    e.bias = ep.bias ? ep.bias + nqk : nullptr;
+    e.out0 = ep.out0 + nqk;
+    e.n_split = ep.n_split - nqk;
+  }
+  return launch_gemm(epi, xn, d, fmt, m->w1[l].rows((size_t)(c0 + nqk) * d), d, M, N - nqk, d, e, st, m);
+}
+
 // zf_last: the fp32 hook_z copy of each sequence's last row only, at row s of zf
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
               Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st, bool zf_last = false,
@@ -730,8 +774,7 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   const tvr_layer_weights& w = m->layers[l];
   TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m));
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
-  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, R, m->D1, d,
-                      e1, st, m));
+  TVR_TRY(launch_w1(m, l, a.xn, R, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
   TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
   ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf ? (zf_last ? n_seqs : std::min(R, zf_rows)) : 0));
@@ -756,13 +799,11 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   kv.out0 = a.qkv + d;
   kv.ld0 = 3 * d;
   kv.n_split = 2 * d;
-  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt,
-                      m->w1[l].rows((size_t)d * d), d, R, 2 * d, d, kv, st, m));
+  TVR_TRY(launch_w1(m, l, a.xn, R, d, 2 * d, kv, st));
   GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);  // all columns for the last rows, gathered and scattered in place
   e1.a_rows = d_last;
   e1.out_rows = d_last;
-  TVR_TRY(launch_gemm(a.fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU, a.xn, d, a.fmt, m->w1[l], d, n_last, m->D1,
-                      d, e1, st, m));
+  TVR_TRY(launch_w1(m, l, a.xn, n_last, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
   TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
   ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? std::min(n_last, zf_rows) : 0));
@@ -884,7 +925,7 @@ int flush_pending(tvr_trace* t, void* stream);
 extern "C" {
 
 const char* tvr_version(void) {
-  return "tvr-mi355x 0.4.0 (gfx950, fp32 MFMA | fp32-accurate 3-plane bf16 / 2-plane fp16 split MFMA | bf16 MFMA)";
+  return "tvr-mi355x 0.5.0 (gfx950, fp32 MFMA | fp32-accurate 3-plane bf16 / 2-plane fp16 split MFMA | bf16 MFMA)";
 }
 int32_t tvr_abi_version(void) { return TVR_ABI_VERSION; }
 const char* tvr_last_error(void) { return g_last_error.c_str(); }
@@ -982,6 +1023,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   // back to plain fp32 operands first (frees the previous mode's planes)
   for (auto& w : m->w1) w = MatW{w.f};
   for (auto& w : m->w2) w = MatW{w.f};
+  m->w1qk.clear();
   m->wu = MatW{m->wu.f};
   if (m->planes) TVR_HIP(hipFree(m->planes));
   m->planes = nullptr;
@@ -998,7 +1040,8 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   const size_t n1 = (size_t)m->D1 * c.d_model, n2 = (size_t)c.d_model * m->K2;
   const size_t nu = (size_t)c.d_vocab * c.d_model;
   const int np = mode == TVR_GEMM_X3BF16 ? 3 : mode == TVR_GEMM_X2F16 ? 2 : 1;
-  const size_t total = np * ((n1 + n2) * L + nu);
+  const size_t nqk = (size_t)2 * c.d_model * c.d_model;  // BF16: W1's Q / K rows as an fp16 plane
+  const size_t total = np * ((n1 + n2) * L + nu) + (mode == TVR_GEMM_BF16 ? nqk * L : 0);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
     (void)hipGetLastError();
@@ -1014,14 +1057,22 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   }
   mats.push_back(&m->wu); sizes.push_back(nu);
   std::vector<float> scale(mats.size(), 1.0f);
-  if (mode == TVR_GEMM_X2F16) {
+  if (mode == TVR_GEMM_BF16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
+    for (int l = 0; l < L; ++l) {
+      mats.push_back(nullptr);
+      sizes.push_back(nqk);
+    }
+  }
+  if (mode == TVR_GEMM_X2F16 || mode == TVR_GEMM_BF16) {
     // one power-of-two scale per matrix from its largest magnitude
     unsigned* d_max = nullptr;
     TVR_HIP(hipMalloc(&d_max, mats.size() * sizeof(unsigned)));
     std::vector<unsigned> h_max(mats.size(), 0);
     hipError_t e = hipMemsetAsync(d_max, 0, mats.size() * sizeof(unsigned), st);
     for (size_t i = 0; i < mats.size() && e == hipSuccess; ++i) {
-      hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, mats[i]->f, sizes[i], d_max + i);
+      const float* src = mats[i] ? mats[i]->f : m->w1[i - (mats.size() - L)].f;  // null: layer's Q / K rows
+      if (mode == TVR_GEMM_BF16 && mats[i]) continue;
+      hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, src, sizes[i], d_max + i);
       e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h_max.data(), d_max, mats.size() * sizeof(unsigned),
@@ -1037,8 +1088,17 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   }
   uint16_t* p = m->planes;
   for (size_t i = 0; i < mats.size(); ++i) {
-    MatW& w = *mats[i];
     const size_t n = sizes[i];
+    if (!mats[i]) {  // BF16: layer l's fp16 Q / K plane (the first 2d rows of W1, row stride d)
+      const int l = (int)(i - (mats.size() - L));
+      const float* f = m->w1[l].f;
+      hipLaunchKernelGGL(f16_plane_kernel, dim3(2048), dim3(256), 0, st, f, scale[i], p, n);
+      TVR_HIP(hipGetLastError());
+      m->w1qk.push_back(MatW{f, nullptr, p, n, scale[i]});
+      p += n;
+      continue;
+    }
+    MatW& w = *mats[i];
     if (mode == TVR_GEMM_X3BF16) {
       hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
       w = MatW{w.f, p, nullptr, n, 1.0f};
@@ -1140,12 +1200,21 @@ int tvr_trace_create(tvr_model* m, int32_t max_seqs, int32_t max_tokens, tvr_tra
 
 int tvr_trace_destroy(tvr_trace* t) {
   if (!t) return TVR_OK;
+  // a deferred clean forward still owes its outputs to the caller: run it
+  // (on the null stream, which orders after the caller's blocking streams)
+  int rc = TVR_OK;
+  if (t->pending) rc = flush_pending(t, nullptr);
   (void)hipDeviceSynchronize();
   if (t->resid) (void)hipFree(t->resid);
   if (t->z) (void)hipFree(t->z);
   if (t->qkv) (void)hipFree(t->qkv);
   delete t;
-  return TVR_OK;
+  return rc;
+}
+
+int tvr_trace_flush(tvr_trace* t, void* stream) {
+  if (!t) return fail(TVR_ERR_INVALID, "tvr_trace_flush: null trace");
+  return flush_pending(t, stream);
 }
 
 int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, void* stream) {
@@ -1647,8 +1716,20 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
       lin_nrows[l] = (int)lin_rows.size() - r_first;
     }
   }
-  const bool any_lin = !lin_mbs.empty();
-  if (any_lin) TVR_TRY(ensure_lin(m, st));
+  bool any_lin = !lin_mbs.empty();
+  if (any_lin) {
+    const int rc = ensure_lin(m, st);
+    if (rc == TVR_ERR_NOMEM) {  // the W1 W_O planes do not fit: the full-GEMM entry (TVR_LIN_ENTRY=0) instead
+      any_lin = false;
+      std::fill(use_lin.begin(), use_lin.end(), 0);
+      lin_vids.clear();
+      lin_rows.clear();
+      lin_mbs.clear();
+      lin_max_nv = 0;
+    } else {
+      TVR_TRY(rc);
+    }
+  }
 
   const int RA = Rc + R;  // rows of the activation buffers
   // run_final chunks: the sites' (logits requested or not) and the fused clean rows' (never logits)
@@ -1778,7 +1859,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     e1.raw = raw_h;
     e1.raw_rows = Rc;
     e1.ld_raw = c.d_mlp;
-    TVR_TRY(launch_gemm(EPI_SPLIT_GELU_ACT, a.xn, d, fmt, m->w1[l], d, Rp, D1, d, e1, st, m));
+    TVR_TRY(launch_w1(m, l, a.xn, Rp, 0, D1, e1, st));
     ProfSpan ps(m, st);
     const bool prof = m->prof;
     m->prof = false;  // G and the entry rows are timed as one HBM-kind span, not as GEMM-family launches

@@ -378,6 +378,9 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+        } else if constexpr (FMT == ACT_F16) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][1], c, 0, 0, 0);
         } else {
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][0], fa[i][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][1], fa[i][1], c, 0, 0, 0);

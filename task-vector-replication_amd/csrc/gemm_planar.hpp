@@ -54,6 +54,11 @@ struct PlanarFmt<ACT_BF16> {
   static constexpr int NPL = 1, BK = 64;
   using frag = bf16x8_t;
 };
+template <>
+struct PlanarFmt<ACT_F16> {  // one fp16 plane (TVR_GEMM_BF16's Q / K columns), v_mfma_f32_16x16x32_f16
+  static constexpr int NPL = 1, BK = 64;
+  using frag = f16x8;
+};
 
 // One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land
 // at lds_base + 16 l.  (A non-template wrapper: referenced directly from a

@@ -106,7 +106,7 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
         const int c = lane + 64 * u;
         const float4 o = make_float4(v[u].x / scale, v[u].y / scale, v[u].z / scale, v[u].w / scale);
         if constexpr (FMT != ACT_F32) {
-          store_act4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, o.x, o.y, o.z, o.w, nullptr);
+          store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, o.x, o.y, o.z, o.w);
         } else {
           ((float4*)((float*)y + (size_t)r * ldy))[c] = o;
         }
@@ -133,7 +133,7 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;
     v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
     if constexpr (FMT != ACT_F32) {
-      store_act4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, v.x, v.y, v.z, v.w, nullptr);
+      store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, v.x, v.y, v.z, v.w);
     } else {
       ((float4*)((float*)y + (size_t)r * ldy))[c] = v;
     }

@@ -44,7 +44,10 @@ __device__ __forceinline__ void wave_argmax(float& bv, int& bi) {
 }
 
 
-enum ActFmt { ACT_F32 = 0, ACT_X2F16 = 1, ACT_BF16 = 2 };
+// ACT_F16: one fp16 plane, read from plane 1 of a TVR_GEMM_BF16 LayerNorm
+// output (store_ln4): the operand format of that mode's attention-score
+// projections (Q, K columns of W1), see engine.hip launch_w1.
+enum ActFmt { ACT_F32 = 0, ACT_X2F16 = 1, ACT_BF16 = 2, ACT_F16 = 3 };
 
 constexpr float X2_ASCALE = 16.0f;
 constexpr float X2_FP16_OVERFLOW = 65520.0f;  // fp16(x) is inf from here (round to nearest)
@@ -111,6 +114,22 @@ __device__ __forceinline__ void store_act4(uint16_t* p, int plane, float a, floa
   }
 }
 
+// LayerNorm outputs (|a| <= sqrt(d): no range check).  TVR_GEMM_BF16 writes
+// fp16(a) into the otherwise unused plane 1 as well: the Q / K projections
+// read it (bf16 rounding of the score operands, amplified by the softmax at
+// peaked attention, was the dominant error of bf16 extraction: 2.7e-2 of
+// max |mean| with bf16 Q / K, 1.4e-2 with fp16 Q / K in a CPU emulation at
+// Pythia-6.9B width, tests/test_gpu_headline_shapes.py's weights).
+template <int FMT>
+__device__ __forceinline__ void store_ln4(uint16_t* p, int plane, float a, float b, float c, float d) {
+  store_act4<FMT>(p, plane, a, b, c, d, nullptr);
+  if constexpr (FMT == ACT_BF16) {
+    const f16x2v lo = __builtin_convertvector(f32x2v{a, b}, f16x2v);
+    const f16x2v hi = __builtin_convertvector(f32x2v{c, d}, f16x2v);
+    *(uint2*)(p + plane) = make_uint2(__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi));
+  }
+}
+
 // eight consecutive elements (p 16-B aligned): one 16-B store per plane
 template <int FMT, bool NT = false>
 __device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (&v)[8], unsigned* flag) {
@@ -152,6 +171,13 @@ __global__ void act_rows_kernel(const float* __restrict__ a, int lda, uint16_t* 
 __global__ void bf16_plane_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     out[i] = bf16_bits(w[i]);
+}
+
+// W [n] fp32 -> one fp16 plane of scale * W (scale a power of two putting
+// max |W| in [2^14, 2^15]: the TVR_GEMM_BF16 Q / K weights, load time)
+__global__ void f16_plane_kernel(const float* __restrict__ w, float scale, uint16_t* __restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = __builtin_bit_cast(uint16_t, (_Float16)(w[i] * scale));
 }
 
 }  // namespace tvr

@@ -103,9 +103,9 @@ def sharded_cie(n_layers: int, n_heads: int, n_prompts: int,
     ``local_fn(heads)`` returns Σ_prompts Δp as [L, H] with zeros outside
     ``heads``."""
     rank, size = world(group)
-    heads = strided_shard(n_heads, rank, size)
-    if not heads:
+    if size > n_heads:  # checked on every rank before any collective: no rank is left waiting in the all-reduce
         raise ValueError("every rank needs at least one head (world size > n_heads)")
+    heads = strided_shard(n_heads, rank, size)
     return all_reduce_sum(local_fn(heads).clone(), group) / n_prompts
 
 

@@ -35,7 +35,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .model import Model, make_sites
+from .model import Model, make_sites, range_checked
 from .prompts import (Pairs, assemble_end_list_tasks, construct_query, generate_shuffled_prompt,  # noqa: F401
                       generate_shuffled_prompts, icl_multi_token, icl_single_token, sample_icl_prompts)
 
@@ -58,6 +58,7 @@ def _chunks(n: int, size: int):
 
 
 # ------------------------------------------------------------------ a1 / a2
+@range_checked
 def generate_mean_activation(contexts: Pairs, function_token: str, seperator_token: str = ",",
                              model: Model = None, num_contexts: int = 1024, len_contexts: int = 4
                              ) -> torch.Tensor:
@@ -69,6 +70,7 @@ def generate_mean_activation(contexts: Pairs, function_token: str, seperator_tok
     return model.project_heads(sum_last_z(model, prompts)) / num_contexts
 
 
+@range_checked
 def sum_last_z(model: Model, prompts: Sequence[Sequence[int]]) -> torch.Tensor:
     """Σ over prompts of hook_z at the last position, [L, d] (fp32, device)."""
     total = None
@@ -93,18 +95,21 @@ def _layer_vectors(layered_vectors: torch.Tensor, model: Model, late_binding: bo
 
 
 def _add_site_outputs(model: Model, seqs: List[List[int]], site_seq, site_layer, site_vec, vectors: torch.Tensor,
-                      targets: Optional[List[int]], topk: int, shard=None):
+                      targets: Optional[List[int]], topk: int, shard=None, clean_outputs: bool = True):
     """Clean forward of ``seqs`` + the ADD_ATTN_OUT_LASTPOS sites
     (``hook_attn_out[0, -1] += vectors[vec]`` at ``layer``, scratch2.py:107-109)
     of the global site list (site_seq, site_layer, site_vec).  ``shard``
     (distributed.SiteShard) evaluates only this rank's sites and all-gathers
     the per-site outputs, so every rank returns every site in global order.
+    ``clean_outputs=False``: the caller reads no clean outputs, so the clean
+    rows skip their final LayerNorm + unembed statistics.
     Returns (clean outputs per prompt, patched outputs per site)."""
     n_sites = len(site_seq)
     sel = np.arange(n_sites) if shard is None else np.asarray(shard.select(n_sites), dtype=np.int64)
     trace = model._sweep_trace(len(seqs), sum(len(s) for s in seqs))
     # the clean rows run inside the first sweep launch when there is one
-    clean = model.forward_clean(seqs, targets=targets, topk=topk, trace=trace, defer=len(sel) > 0)
+    clean = model.forward_clean(seqs, targets=targets if clean_outputs else None, topk=topk if clean_outputs else 0,
+                                trace=trace, defer=len(sel) > 0)
     dev = model.device
     patched = {}
     if targets is not None:
@@ -131,24 +136,26 @@ def _add_site_outputs(model: Model, seqs: List[List[int]], site_seq, site_layer,
 
 
 def _injection_sweep(model: Model, seqs: List[List[int]], vectors: torch.Tensor, vec_of_layer,
-                     layers: Sequence[int], targets: Optional[List[int]], topk: int, shard=None):
+                     layers: Sequence[int], targets: Optional[List[int]], topk: int, shard=None,
+                     clean_outputs: bool = True):
     """One ADD_ATTN_OUT_LASTPOS site per (prompt, layer).  Returns (clean
     outputs, patched outputs [n, len(layers)])."""
     n, layers = len(seqs), list(layers)
     site_layer = np.tile(np.asarray(layers, dtype=np.int32), n)
     clean, patched = _add_site_outputs(model, seqs, np.repeat(np.arange(n, dtype=np.int32), len(layers)), site_layer,
                                        np.asarray([vec_of_layer(l) for l in site_layer], dtype=np.int32), vectors,
-                                       targets, topk, shard)
+                                       targets, topk, shard, clean_outputs)
     return clean, {k: v.view(n, len(layers), *v.shape[1:]) for k, v in patched.items()}
 
 
+@range_checked
 def _zero_shot_accuracy(layered_vectors, contexts: Pairs, function_token: str, model: Model,
                         reference_late_binding: bool, shard=None) -> List[float]:
     L = model.cfg.n_layers
     vectors, vec_of = _layer_vectors(layered_vectors, model, reference_late_binding)
     f = model.to_single_token(function_token)
     seqs = [[0, model.to_single_token(x), f] for x, _ in contexts]
-    _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, 1, shard)
+    _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, 1, shard, clean_outputs=False)
     top1 = patched["topk"][..., 0].cpu().tolist()
     hits = [0] * L
     for (x, y), row in zip(contexts, top1):
@@ -157,6 +164,7 @@ def _zero_shot_accuracy(layered_vectors, contexts: Pairs, function_token: str, m
     return [1.0 * h / len(contexts) for h in hits]
 
 
+@range_checked
 def _zero_shot_dprob(layered_vectors, contexts: Pairs, function_token: str, model: Model,
                      reference_late_binding: bool, shard=None) -> torch.Tensor:
     L = model.cfg.n_layers
@@ -169,6 +177,7 @@ def _zero_shot_dprob(layered_vectors, contexts: Pairs, function_token: str, mode
     return (patched["prob"] - clean["prob"][:, None]).sum(0) / len(contexts)
 
 
+@range_checked
 def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: Pairs, function_token: str,
                                        model: Model = None, reference_late_binding: bool = True) -> List[float]:
     """Per-layer top-1 accuracy of zero-shot ``[BOS, x, f]`` prompts with a
@@ -176,6 +185,7 @@ def apply_layered_vectors_to_zero_shot(layered_vectors: torch.Tensor, contexts: 
     return _zero_shot_accuracy(layered_vectors, contexts, function_token, model, reference_late_binding)
 
 
+@range_checked
 def apply_layered_vectors_to_zero_shot_by_probability(layered_vectors: torch.Tensor, contexts: Pairs,
                                                       function_token: str, model: Model = None,
                                                       reference_late_binding: bool = True) -> torch.Tensor:
@@ -195,6 +205,7 @@ def normalize_cie_inputs(model: Model, scrambled_prompts, prompt_answers):
     return prompts, answers
 
 
+@range_checked
 def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Sequence[Sequence[int]],
                                 answers: Sequence[int], model: Model,
                                 layers: Optional[Sequence[int]] = None,
@@ -233,6 +244,7 @@ def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Se
     return out
 
 
+@range_checked
 def calculate_average_causal_indirect_effect(mean_head_activations: torch.Tensor, scrambled_prompts,
                                              prompt_answers, model: Model = None) -> torch.Tensor:
     """CIE[l, h] = mean over prompts of softmax(patched)[answer[0]] −
@@ -272,7 +284,8 @@ def _fv_topk(task_vector, layer: int, contexts: Pairs, topk: int, model: Model, 
     seqs = [model.to_tokens(x + ":")[0].tolist() for x, _ in contexts]
     firsts = [model.to_string(model.tokenizer.encode(y)[0]) for _, y in contexts]
     vec = task_vector.to(model.device, torch.float32).reshape(1, -1).contiguous()
-    clean, patched = _injection_sweep(model, seqs, vec, lambda l: 0, [layer], None, topk=topk)
+    clean, patched = _injection_sweep(model, seqs, vec, lambda l: 0, [layer], None, topk=topk,
+                                      clean_outputs=with_baseline)
     def hits(top):
         return sum(first in [model.to_string(t) for t in row] for first, row in zip(firsts, top.tolist()))
     fv = hits(patched["topk"][:, 0].cpu())
@@ -280,6 +293,7 @@ def _fv_topk(task_vector, layer: int, contexts: Pairs, topk: int, model: Model, 
     return base, fv
 
 
+@range_checked
 def check_accuracy_of_task_vector(task_vector: torch.Tensor, layer: int, contexts: Pairs, topk: int = 5,
                                   model: Model = None) -> Tuple[float, float]:
     """(zero-shot top-k accuracy, top-k accuracy with the FV added to
@@ -288,6 +302,7 @@ def check_accuracy_of_task_vector(task_vector: torch.Tensor, layer: int, context
     return (1.0 * base / len(contexts), 1.0 * fv / len(contexts))
 
 
+@range_checked
 def check_accuracy_of_added_task_vector(task_vector: torch.Tensor, layer: int, contexts: Pairs, topk: int = 5,
                                         model: Model = None) -> float:
     _, fv = _fv_topk(task_vector, layer, contexts, topk, model, False)
@@ -295,6 +310,7 @@ def check_accuracy_of_added_task_vector(task_vector: torch.Tensor, layer: int, c
 
 
 # ---------------------------------------------------------------------- a12
+@range_checked
 def test_component_hypothesis(contexts: Pairs, function_token: str, model: Model = None,
                               num_contexts: int = 256, len_contexts: int = 4, batch_contexts: int = 512):
     """Layer sweep of residual patching: the ICL run's ``hook_resid_pre[L][-2]``
@@ -336,6 +352,7 @@ def test_component_hypothesis(contexts: Pairs, function_token: str, model: Model
     return (num_contexts, base_hits, normal_hits, per_layer)
 
 
+@range_checked
 def substitute_task(taskA: Pairs, taskB: Pairs, layer: int, function_token: str = "→", model: Model = None,
                     num_contexts: int = 256, len_contexts: int = 4):
     """Swap ``hook_resid_pre[layer][-1]`` between a task-A and a task-B run of
@@ -388,7 +405,7 @@ def _fv_sites_topk(model: Model, contexts: Pairs, vectors: torch.Tensor, layer_v
     lv = np.asarray(layer_vec, dtype=np.int32).reshape(m, 2)
     vecs = vectors.to(model.device, torch.float32).reshape(-1, model.cfg.d_model).contiguous()
     _, patched = _add_site_outputs(model, seqs, np.repeat(np.arange(n, dtype=np.int32), m), np.tile(lv[:, 0], n),
-                                   np.tile(lv[:, 1], n), vecs, None, topk, shard)
+                                   np.tile(lv[:, 1], n), vecs, None, topk, shard, clean_outputs=False)
     top = patched["topk"].view(n, m, topk).cpu().tolist()
     hits = np.zeros(m, dtype=np.int64)
     for i, first in enumerate(firsts):
@@ -397,6 +414,7 @@ def _fv_sites_topk(model: Model, contexts: Pairs, vectors: torch.Tensor, layer_v
     return hits
 
 
+@range_checked
 def check_accuracy_of_added_task_vector_by_layer(task_vector: torch.Tensor, contexts: Pairs, topk: int = 5,
                                                  model: Model = None, shard=None) -> List[float]:
     """``check_accuracy_of_added_task_vector`` at every layer (one sweep;
@@ -406,6 +424,7 @@ def check_accuracy_of_added_task_vector_by_layer(task_vector: torch.Tensor, cont
     return [float(h) / len(contexts) for h in hits]
 
 
+@range_checked
 def function_vector_head_count_grid(mean_head_activations: torch.Tensor, causal_indirect_effects: torch.Tensor,
                                     contexts: Pairs, model: Model = None, heads_per_batch: int = 2,
                                     number_of_batches: int = 64, topk: int = 5, shard=None) -> torch.Tensor:
@@ -419,18 +438,24 @@ def function_vector_head_count_grid(mean_head_activations: torch.Tensor, causal_
     L, H = model.cfg.n_layers, model.cfg.n_heads
     d = mean_head_activations.shape[-1]
     vecs = [torch.zeros(d, dtype=torch.float32, device=model.device)]  # vector 0: the skipped cells
-    cells = []
+    cells = []  # (i, j, index of the evaluated (layer, vector) pair)
+    pairs = []
     for i in range(L):
+        zero_pair = None  # layer i's skipped cells share ONE (layer i, zero vector) evaluation
         for j in range(number_of_batches):
             k = (j + 1) * heads_per_batch
             if k < (i + 1) * H:
                 vecs.append(assemble_task_vector(mean_head_activations, causal_indirect_effects, i, k)
                             .to(model.device, torch.float32))
-                cells.append((i, j, len(vecs) - 1))
+                pairs.append((i, len(vecs) - 1))
+                cells.append((i, j, len(pairs) - 1))
             else:
-                cells.append((i, j, 0))
-    hits = _fv_sites_topk(model, contexts, torch.stack(vecs), [(i, v) for i, _, v in cells], topk, shard)
+                if zero_pair is None:
+                    pairs.append((i, 0))
+                    zero_pair = len(pairs) - 1
+                cells.append((i, j, zero_pair))
+    hits = _fv_sites_topk(model, contexts, torch.stack(vecs), pairs, topk, shard)
     acc = torch.zeros(L, number_of_batches)
-    for (i, j, _), h in zip(cells, hits):
-        acc[i, j] = float(h) / len(contexts)
+    for i, j, q in cells:
+        acc[i, j] = float(hits[q]) / len(contexts)
     return acc

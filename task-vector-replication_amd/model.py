@@ -9,12 +9,22 @@ token helpers, and drives the engine's batched entry points:
   launch sequence (replaces the per-site ``run_with_hooks`` loops);
 * ``project_heads``  — z-form capture → ``hook_result`` form.
 
-All device work is enqueued on torch's current stream; nothing here has a
-CPU fallback (the engine refuses to run without a GPU).
+The compute entry points run as torch.library operators (``torch.ops.tvr.*``,
+csrc/torch_ops.cpp over the C ABI) on torch's current stream, with outputs
+from torch's allocator; nothing here has a CPU fallback (the engine refuses to
+run without a GPU).
+
+The x2f16 range check (include/tvr.h ``tvr_model_range_status``) reads a
+device-side sticky flag and synchronises: a direct call checks after itself,
+an experiment function (``range_checked``) once at its end, so its sweeps
+enqueue back to back.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
+import inspect
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -28,6 +38,25 @@ from .weights import (EngineWeights, config_from_hf_json, load_hf_safetensors, p
                       synth_engine_weights)
 
 SITE_DTYPE = np.dtype([(f, np.int32) for f in _lib.SITE_FIELDS])
+
+
+def range_checked(fn):
+    """Run ``fn`` (an experiment function taking ``model``) inside the model's
+    range scope: the x2f16 range flag is read once when the outermost scope
+    ends instead of after every engine call."""
+    sig = inspect.signature(fn)
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        try:
+            model = sig.bind_partial(*args, **kwargs).arguments.get("model")
+        except TypeError:  # a bad call: let fn raise its own error
+            model = None
+        if not isinstance(model, Model):
+            return fn(*args, **kwargs)
+        with model.range_scope(fn.__name__):
+            return fn(*args, **kwargs)
+    return wrapper
 
 
 def make_sites(n: int) -> np.ndarray:
@@ -72,9 +101,18 @@ class Trace:
         self._pending_out = None
         return buf
 
+    def flush(self) -> None:
+        """Run a pending deferred clean forward now (its prob / top-k tensors
+        are written; include/tvr.h tvr_trace_flush)."""
+        if self._pending_out is not None:
+            _lib.check(self._lib.tvr_trace_flush(self._h, self.model._stream()), "tvr_trace_flush")
+            self._pending_out = None
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
+            if getattr(self, "_pending_out", None) is not None:
+                self.flush()  # the deferred outputs are owed to the caller (tvr_trace_destroy would also run it)
             self._lib.tvr_trace_destroy(h)
             self._h = None
 
@@ -88,7 +126,9 @@ class Model(TokenizerMixin):
     def __init__(self, cfg: PythiaConfig, weights: EngineWeights, tokenizer=None,
                  device: Optional[torch.device] = None, gemm: str = DEFAULT_GEMM):
         self._h = None
+        self._range_depth = 0
         self._lib = _lib.load()
+        self._ops = _lib.load_ops()
         dev = torch.device(device) if device is not None else weights.w_embed.device
         if dev.type != "cuda" or not torch.cuda.is_available():
             raise _lib.EngineError("the HIP engine needs a GPU device (no CPU fallback): "
@@ -178,11 +218,36 @@ class Model(TokenizerMixin):
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def _check_range(self, what: str) -> None:
+    def _check_range(self, what: str, force: bool = False) -> None:
         """x2f16 only: fail loudly if a GEMM input left the fp16 split's range
-        (synchronises the stream)."""
-        if self.gemm == "x2f16":
+        since the last check (synchronises the stream).  Inside a
+        ``range_scope`` the check waits for the scope's end."""
+        if self.gemm == "x2f16" and (force or self._range_depth == 0):
             _lib.check(self._lib.tvr_model_range_status(self._h, self._stream()), what)
+
+    @contextlib.contextmanager
+    def range_scope(self, what: str):
+        """Defer the per-call range checks of the engine calls inside to ONE
+        check when the outermost scope exits normally (the flag is sticky on
+        the device, so nothing is missed; an exception propagates unchecked)."""
+        self._range_depth += 1
+        try:
+            yield self
+        except BaseException:
+            self._range_depth -= 1
+            raise
+        self._range_depth -= 1
+        self._check_range(what)
+
+    def _op(self, name: str, *args):
+        """torch.ops.tvr.<name>: engine errors as EngineError (invalid
+        arguments stay ValueError, the reference's error type)."""
+        try:
+            return getattr(self._ops, name)(*args)
+        except ValueError:
+            raise
+        except RuntimeError as e:
+            raise _lib.EngineError(str(e)) from e
 
     def trace(self, n_seqs: int, n_tokens: int) -> Trace:
         """A new trace with this capacity, owned by the caller (the experiment
@@ -193,6 +258,8 @@ class Model(TokenizerMixin):
         """The experiment functions' scratch trace (grown on demand, reused)."""
         t = self._trace_cache
         if t is None or t.max_seqs < n_seqs or t.max_tokens < n_tokens:
+            if t is not None:
+                t.flush()  # a deferral on the old trace still owes its outputs
             self._trace_cache = None
             t = Trace(self, max(n_seqs, 1), max(n_tokens, 1))
             self._trace_cache = t
@@ -224,44 +291,31 @@ class Model(TokenizerMixin):
             tg = np.asarray([-1 if t is None else int(t) for t in targets], dtype=np.int32)
             if tg.shape[0] != n:
                 raise ValueError("targets must have one entry per prompt")
-        dev = self.device
-        out = {}
-        prob = torch.empty(n, device=dev) if tg is not None else None
-        top = torch.empty(n, topk, dtype=torch.int32, device=dev) if topk else None
-        logits = torch.empty(n, self.cfg.d_vocab, device=dev) if return_logits else None
-        zsum = torch.zeros(self.cfg.n_layers, self.cfg.d_model, device=dev) if capture else None
         if trace is not None and (trace.max_seqs < n or trace.max_tokens < int(lens.sum())):
             raise ValueError("trace too small for this batch")
-        if defer:
-            if trace is None or logits is not None or zsum is not None:
-                raise ValueError("defer needs a trace and no logits / capture")
-            rc = self._lib.tvr_forward_clean_deferred(
-                self._h, trace._h, toks.ctypes.data, lens.ctypes.data, n,
-                tg.ctypes.data if tg is not None else None, _lib.ptr(prob), _lib.ptr(top), topk, self._stream())
-            _lib.check(rc, "tvr_forward_clean_deferred")
-            trace.seq_lens = lens.tolist()
-            trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
-            trace._pending_out = (prob, top)
-            return {k: v for k, v in (("prob", prob), ("topk", top)) if v is not None}
-        rc = self._lib.tvr_forward_clean(
-            self._h, trace._h if trace is not None else None,
-            toks.ctypes.data, lens.ctypes.data, n,
-            tg.ctypes.data if tg is not None else None,
-            _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits), _lib.ptr(zsum), self._stream())
-        _lib.check(rc, "tvr_forward_clean")
-        self._check_range("tvr_forward_clean")
-        if trace is not None:
-            trace._pending_out = None
-            trace.seq_lens = lens.tolist()
-            trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
-        if prob is not None:
+        if defer and (trace is None or return_logits or capture):
+            raise ValueError("defer needs a trace and no logits / capture")
+        cfg = self.cfg
+        prob, top, logits, zsum = self._op(
+            "forward_clean", self._h.value, trace._h.value if trace is not None else 0, torch.from_numpy(toks),
+            torch.from_numpy(lens), torch.from_numpy(tg) if tg is not None else None, topk, return_logits, capture,
+            defer, cfg.n_layers, cfg.d_model, cfg.d_vocab, self.device)
+        out = {}
+        if tg is not None:
             out["prob"] = prob
-        if top is not None:
+        if topk:
             out["topk"] = top
-        if logits is not None:
+        if return_logits:
             out["logits"] = logits
-        if zsum is not None:
+        if capture:
             out["zsum"] = zsum
+        if trace is not None:
+            trace.seq_lens = lens.tolist()
+            trace.seq_offsets = np.concatenate([[0], np.cumsum(lens)[:-1]]).tolist()
+            # a deferred forward's outputs are written by the next sweep on the trace: keep them alive
+            trace._pending_out = (prob, top) if defer else None
+        if not defer:
+            self._check_range("tvr_forward_clean")
         return out
 
     def patch_sweep(self, trace: Trace, sites: np.ndarray, vectors: Optional[torch.Tensor] = None,
@@ -272,38 +326,30 @@ class Model(TokenizerMixin):
         n = int(sites.shape[0])
         if n == 0:
             raise ValueError("no patch sites")
-        nvec = 0
         if vectors is not None:
             if vectors.device != self.device or vectors.dtype != torch.float32:
                 raise ValueError("vectors must be fp32 on the model device")
             vectors = vectors.reshape(-1, self.cfg.d_model).contiguous()
-            nvec = vectors.shape[0]
-        dev = self.device
-        prob = torch.empty(n, device=dev) if want_prob else None
-        top = torch.empty(n, topk, dtype=torch.int32, device=dev) if topk else None
-        logits = torch.empty(n, self.cfg.d_vocab, device=dev) if return_logits else None
-        rc = self._lib.tvr_patch_sweep(self._h, trace._h, sites.ctypes.data, n, _lib.ptr(vectors), nvec,
-                                       _lib.ptr(prob), _lib.ptr(top), topk, _lib.ptr(logits),
-                                       self._stream())
-        _lib.check(rc, "tvr_patch_sweep")
+        rows = torch.from_numpy(sites.view(np.int32).reshape(n, len(_lib.SITE_FIELDS)))
+        prob, top, logits = self._op("patch_sweep", self._h.value, trace._h.value, rows, vectors, topk, want_prob,
+                                     return_logits, self.cfg.d_vocab, self.device)
         self._check_range("tvr_patch_sweep")
         trace._pending_out = None
         out = {}
-        if prob is not None:
+        if want_prob:
             out["prob"] = prob
-        if top is not None:
+        if topk:
             out["topk"] = top
-        if logits is not None:
+        if return_logits:
             out["logits"] = logits
         return out
 
     def project_heads(self, zsum: torch.Tensor) -> torch.Tensor:
         """[L, d] z-sums → [L, H, d] hook_result sums."""
-        zsum = zsum.contiguous()
-        out = torch.empty(self.cfg.n_layers, self.cfg.n_heads, self.cfg.d_model, device=self.device)
-        _lib.check(self._lib.tvr_project_heads(self._h, zsum.data_ptr(), out.data_ptr(), self._stream()),
-                   "tvr_project_heads")
-        return out
+        if tuple(zsum.shape) != (self.cfg.n_layers, self.cfg.d_model):
+            raise ValueError("zsum must be [n_layers, d_model]")
+        return self._op("project_heads", self._h.value, zsum.to(self.device, torch.float32).contiguous(),
+                        self.cfg.n_heads)
 
     # ------------------------------------------------------------ profiling
     def profile(self, on: bool) -> None:
@@ -354,9 +400,8 @@ class Model(TokenizerMixin):
             if last_only:
                 return self.forward_clean([ids], return_logits=True)["logits"].view(1, 1, -1)
             toks, lens = self._pack([ids])
-            out = torch.empty(len(ids), V, device=dev)
-            rc = self._lib.tvr_forward_logits(self._h, toks.ctypes.data, None, 0, lens.ctypes.data, 1,
-                                              out.data_ptr(), self._stream())
+            out = self._op("forward_logits", self._h.value, torch.from_numpy(toks), None, 0, torch.from_numpy(lens),
+                           V, dev)
         else:
             resid = torch.as_tensor(tokens).to(dev, torch.float32)
             if resid.dim() == 3:
@@ -367,10 +412,8 @@ class Model(TokenizerMixin):
                 raise ValueError("start_at_layer needs a residual of shape [1, T, d_model]")
             resid = resid.contiguous()
             lens = np.asarray([resid.shape[0]], dtype=np.int32)
-            out = torch.empty(resid.shape[0], V, device=dev)
-            rc = self._lib.tvr_forward_logits(self._h, None, resid.data_ptr(), int(start_at_layer), lens.ctypes.data,
-                                              1, out.data_ptr(), self._stream())
-        _lib.check(rc, "tvr_forward_logits")
+            out = self._op("forward_logits", self._h.value, None, resid, int(start_at_layer), torch.from_numpy(lens),
+                           V, dev)
         self._check_range("tvr_forward_logits")
         if last_only:
             out = out[-1:]

@@ -18,7 +18,7 @@ def declared_functions():
 def test_header_declares_the_entry_points():
     names = declared_functions()
     for want in ("tvr_model_create", "tvr_forward_clean", "tvr_patch_sweep", "tvr_project_heads",
-                 "tvr_trace_create", "tvr_trace_read", "tvr_gemm_f32"):
+                 "tvr_trace_create", "tvr_trace_read", "tvr_trace_flush", "tvr_gemm_f32"):
         assert want in names
 
 
@@ -34,7 +34,7 @@ def test_binding_covers_header():
 
 def test_version_and_errors_without_gpu():
     lib = tvr_amd._lib.load()
-    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 8
+    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 9
     assert b"gfx950" in lib.tvr_version()
     # argument validation runs before any device call
     out = ctypes.c_void_p()
@@ -59,3 +59,33 @@ def test_model_refuses_cpu_device(tiny_cfg):
     w = tvr_amd.weights.synth_engine_weights(tiny_cfg, seed=0)
     with pytest.raises(tvr_amd._lib.EngineError, match="no CPU fallback"):
         tvr_amd.Model(tiny_cfg, w)
+
+
+# the façade calls torch.ops.tvr.*, registered by _tvr_ops.so over the C ABI
+OP_SCHEMAS = {
+    "forward_clean": "tvr::forward_clean(int model, int trace, Tensor tokens, Tensor seq_lens, Tensor? targets, "
+                     "int topk, bool want_logits, bool capture, bool defer, int n_layers, int d_model, int d_vocab, "
+                     "Device device) -> (Tensor, Tensor, Tensor, Tensor)",
+    "patch_sweep": "tvr::patch_sweep(int model, int trace, Tensor sites, Tensor? vectors, int topk, bool want_prob, "
+                   "bool want_logits, int d_vocab, Device device) -> (Tensor, Tensor, Tensor)",
+    "project_heads": "tvr::project_heads(int model, Tensor zsum, int n_heads) -> Tensor",
+    "forward_logits": "tvr::forward_logits(int model, Tensor? tokens, Tensor? resid, int start_layer, "
+                      "Tensor seq_lens, int d_vocab, Device device) -> Tensor",
+}
+
+
+def test_torch_ops_schemas():
+    ops = tvr_amd._lib.load_ops()
+    assert set(OP_SCHEMAS) == set(tvr_amd._lib.OPS)
+    for name, schema in OP_SCHEMAS.items():
+        assert str(getattr(ops, name).default._schema) == schema
+
+
+def test_torch_ops_refuse_cpu_and_bad_arguments():
+    import pytest
+    import torch
+    ops = tvr_amd._lib.load_ops()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.project_heads(1, torch.zeros(2, 4), 2)
+    with pytest.raises(ValueError, match=r"\[n_sites, 9\]"):
+        ops.patch_sweep(1, 1, torch.zeros(3, 8, dtype=torch.int32), None, 0, True, False, 8, torch.device("cuda", 0))

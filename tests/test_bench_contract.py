@@ -53,3 +53,21 @@ def test_hbm_kernels_pmc_traffic_keyed_on_workload():
             assert out[k]["traffic"] == v["fetch_bytes_x2_per_launch"] + v["write_bytes_per_launch"]
     other = bench.hbm_kernels(hbm, None, steps=2, workload="another workload")
     assert all("traffic" not in (other[k] or {}) for k in ("entry", "lnpre", "attention", "row_stats"))
+
+
+def test_gpus_flag_launches_ranks_itself():
+    """``bench.py --gpus 2`` without torchrun starts 2 ranks of itself (the
+    parent never touches a GPU) and rank 0 reports the world size the process
+    group saw (--gpus was parsed and ignored)."""
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(bench.ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--launch-check"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["launch_check"]
+    assert len(out["rank_elapsed_s"]) == 2 and out["max_elapsed_s"] == max(out["rank_elapsed_s"])

@@ -22,8 +22,8 @@ extraction (a1), both layer sweeps (a4 accuracy, a5 Δprob), the CIE over every
 (layer, head) site of every prompt (a7), the FV top-5 accuracy (a10, a11).
 Tolerances: fp32 paths as tests/test_gpu_engine.py (1e-4 relative on logits
 and vectors, |Δ| <= 1e-4 max|ref| + 1e-7 on probabilities / CIE, accuracies and
-top-k identical); bf16 at the north star's 2e-2 (extracted vectors Frobenius-
-relative, logits max-relative), probabilities and CIE within 5e-2 of the
+top-k identical); bf16 at the north star's 2e-2 (extracted vectors and logits
+max-abs relative, the fp32 paths' metric), probabilities and CIE within 5e-2 of the
 largest probability involved (bf16's own rounding), accuracies within 0.1.
 """
 import random
@@ -131,17 +131,18 @@ def test_headline_width_parity(width, gemm):
         random.seed(2)
         mean = tvr_amd.generate_mean_activation(list(tvr_amd.tasks.letter_to_caps), ARROW, ",", model=model,
                                                 num_contexts=16, len_contexts=6)
-        if bf16:  # the vectors as a whole (Frobenius): max-abs is 2.6e-2 of max |mean| at std-0.1 weights
-            print(f"bf16 extraction: max-abs rel {rel_err(mean, r['mean']):.3e}, "
-                  f"frobenius rel {fro_err(mean, r['mean']):.3e}")
-            assert fro_err(mean, r["mean"]) < tol
-        else:
-            assert rel_err(mean, r["mean"]) < tol
+        # the same metric on every path: max-abs error relative to max |mean| (bf16: the north star's 2e-2;
+        # the Q / K projections run on fp16 operands in the bf16 mode, csrc/split.hpp store_ln4)
+        print(f"{gemm} extraction: max-abs rel {rel_err(mean, r['mean']):.3e}, "
+              f"frobenius rel {fro_err(mean, r['mean']):.3e}")
+        assert rel_err(mean, r["mean"]) < tol
         # a4 / a5 on the oracle's means (each function isolated)
         layered = tvr_amd.gather_head_activations_to_layers(r["mean"].cuda())
         acc = tvr_amd.apply_layered_vectors_to_zero_shot(layered, r["arrow"], ARROW, model=model)
         dp = tvr_amd.apply_layered_vectors_to_zero_shot_by_probability(layered, r["arrow"], ARROW, model=model)
         if bf16:
+            print(f"bf16 layer sweeps: accuracy {acc} vs {r['acc']}, max |d dprob| "
+                  f"{(dp.cpu().double() - r['dprob'].double()).abs().max().item():.3e}")
             assert max(abs(a - b) for a, b in zip(acc, r["acc"])) <= 0.1, (acc, r["acc"])
             assert (dp.cpu().double() - r["dprob"].double()).abs().max().item() <= BF16_PROB_TOL
         else:
@@ -153,6 +154,7 @@ def test_headline_width_parity(width, gemm):
         cie = sums.cpu().double() / len(r["prompts"])
         err = (cie - r["cie"].double()).abs().max().item()
         if bf16:  # bf16 rounding of the GEMM inputs on std-6 logits: ~2.7e-2 of p at p = 0.91
+            print(f"bf16 CIE: max abs err {err:.3e} = {err / pmax:.3e} of p_max {pmax:.3f}")
             assert err <= BF16_PROB_TOL * pmax, (err, pmax)
         else:
             assert err <= tol * r["cie"].abs().max().item() + 1e-7, (err, r["cie"].abs().max().item())
