@@ -106,6 +106,10 @@ def parse():
     ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks on one GPU")
+    ap.add_argument("--configs", default="C2,C5",
+                    help="N=1: the other BASELINE.json configs timed after the headline, reported under 'configs' "
+                         "(C2 = the Pythia-2.8B layer sweeps on the headline model, C5 = the Pythia-12B 36x40 "
+                         "10-shot CIE sweep); '' skips them")
     ap.add_argument("--launch-check", dest="launch_check", action="store_true",
                     help="only the rank launch, rendezvous and max-over-ranks timing (no GPU work; CPU test)")
     return ap.parse_args()
@@ -217,6 +221,77 @@ def hbm_kernels(hbm, hbm_ex, steps, workload=None):
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _sync_time(fn, reps):
+    """fn() run `reps` times between synchronize calls; seconds per call."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, out
+
+
+def config_c2(model, mean, peak, reps=3):
+    """C2: the per-layer accuracy and Δprob sweeps of a 52-pair
+    task over all layers (52 zero-shot [BOS, x, f] prompts x L layers = 1,664
+    ADD_ATTN_OUT_LASTPOS sites per sweep, scratch2.py:114-150), with the
+    layer-(L-1) vector of the headline's 2048-prompt extraction (late binding,
+    App. B1).  Roofline: F_alg = (L-1-l)(2 P_l + 4 T0 d) + 2 d V per site,
+    averaged over l (T0 = 3)."""
+    import tvr_amd
+    from tvr_amd import experiments as E
+    cfg = model.cfg
+    L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
+    P_l = 4 * d * d + 2 * d * cfg.d_mlp
+    f_alg = sum((L - 1 - l) * (2 * P_l + 4 * 3 * d) + 2 * d * V for l in range(L)) / L
+    task = tvr_amd.tasks.letter_to_caps
+    lv = E.gather_head_activations_to_layers(mean)
+    out = {"workload": f"{len(task)} zero-shot prompts (T0=3) x {L} layers = {len(task) * L} sites per sweep, "
+                       "vector = layer-(L-1) sum of the headline's extraction means",
+           "gflop_per_site": round(f_alg / 1e9, 3), "reps": reps}
+    for key, fn in (("accuracy", lambda: E.apply_layered_vectors_to_zero_shot(lv, task, tvr_amd.tasks.ARROW, model)),
+                    ("dprob", lambda: E.apply_layered_vectors_to_zero_shot_by_probability(lv, task, tvr_amd.tasks.ARROW,
+                                                                                          model))):
+        fn()  # warm (trace / workspace sizing)
+        sec, _ = _sync_time(fn, reps)
+        rate = len(task) * L / sec
+        out[key] = {"ms_per_sweep": round(sec * 1e3, 3), "sites_per_s": round(rate, 1),
+                    "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak, 4)}
+    return out
+
+
+def config_c5(args, dev, peak):
+    """C5: Pythia-12B, the full 36 x 40 CIE sweep of 12
+    shuffled 10-shot prompts (T = 33): 17,280 patched prompts per step on one
+    GPU (the 8-GPU run shards heads as the headline does).  Seeded synthetic
+    weights and means; one warmup step, `steps` timed.  F_alg per SURVEY §8d."""
+    import tvr_amd
+    from tvr_amd.experiments import causal_indirect_effect_sums
+    t0 = time.time()
+    model = tvr_amd.Model.from_pretrained("pythia-12b", device=dev, seed=0, gemm=args.gemm)
+    cfg = model.cfg
+    g = torch.Generator(device=dev).manual_seed(4321)
+    mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
+    prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, 10, seed=1234)
+    build_s = time.time() - t0
+    step = lambda: causal_indirect_effect_sums(mean, prompts, answers, model)  # noqa: E731
+    step()
+    steps = max(1, min(args.steps, 2))
+    sec, _ = _sync_time(step, steps)
+    L, d, V, T = cfg.n_layers, cfg.d_model, cfg.d_vocab, len(prompts[0])
+    P_l = 4 * d * d + 2 * d * cfg.d_mlp
+    f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
+    units = len(prompts) * L * cfg.n_heads
+    rate = units / sec
+    del model
+    torch.cuda.empty_cache()
+    return {"workload": f"pythia-12b CIE sweep {L}x{cfg.n_heads} sites, {len(prompts)} prompts/step, 10-shot, T={T}",
+            "units_per_step": units, "steps": steps, "ms_per_step": round(sec * 1e3, 1),
+            "value": round(rate, 2), "unit": "patched prompts/s", "gflop_per_site": round(f_alg / 1e9, 2),
+            "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak, 4),
+            "model_build_s": round(build_s, 1)}
 
 
 def cpu_baseline(args, cfg, prompts, answers, mean, model):
@@ -503,6 +578,25 @@ def main():
         out["emulated_world"] = emulate
     if rank == 0 and world == 1 and args.cpu_baseline and not emulate:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
+    which = {c for c in args.configs.split(",") if c} if world == 1 and not emulate and args.model == "pythia-2.8b" \
+        else set()
+    if which:  # the other BASELINE.json configs, timed after the headline (not part of `value`)
+        out["configs"] = {}
+        if "C2" in which:
+            try:
+                out["configs"]["C2"] = config_c2(model, mean, peak)
+                log(f"C2: {out['configs']['C2']['accuracy']['sites_per_s']} / {out['configs']['C2']['dprob']['sites_per_s']} sites/s")
+            except Exception as e:  # a config leg never voids the headline line
+                out["configs"]["C2"] = {"error": f"{type(e).__name__}: {e}"}
+        if "C5" in which:
+            del model
+            torch.cuda.empty_cache()
+            model = None
+            try:
+                out["configs"]["C5"] = config_c5(args, dev, peak)
+                log(f"C5: {out['configs']['C5']['value']} patched prompts/s")
+            except Exception as e:
+                out["configs"]["C5"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -5,7 +5,7 @@
 TAG=${1:?tag}; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread "$@" \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread "$@" \
     > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?
 tail -4 gpurun_out/gpu_tests_$TAG.log
