@@ -381,19 +381,85 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
   return TVR_OK;
 }
 
+// Stream-K over tiles [tile_base, tile_base + count): G blocks share their
+// k-iterations evenly (gemm_pingpong_kernel sk_blocks), fp32 partial tiles to
+// the model's split-K workspace, then splitk_sk_reduce_kernel sums each tile's
+// partials in k order and applies the epilogue (deterministic).
+int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
+                 const GemmEpi& ep0, float acc_scale, int tile_base, int count, int G, tvr_model* m, hipStream_t st) {
+  const int rc = ensure_splitk(m, (size_t)2 * G * PP_TILE_ELEMS * sizeof(float), st);
+  if (rc != TVR_OK) return rc;
+  GemmEpi ep = ep0;
+  ep.group_m = pp_group_m(N);
+  GemmEpi pe{};
+  pe.group_m = ep.group_m;
+  pe.out0 = m->splitk_ws;
+  pe.a_rows = ep.a_rows;
+  pe.sk_blocks = G;
+  pe.tile_base = tile_base;
+  pe.tile_count = count;
+  const dim3 g(G), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
+  if (a_fmt == ACT_X2F16)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_F16)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+                       (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  const int KT = K / (a_fmt == ACT_X2F16 ? 32 : 64);
+#define TVR_SKR(E, F)                                                                                         \
+  hipLaunchKernelGGL((splitk_sk_reduce_kernel<E, F>), rg, dim3(256), 0, st, (const float*)m->splitk_ws, G, KT, \
+                     tile_base, count, M, N, ep)
+#define TVR_SKR_F(E) \
+  if (a_fmt == ACT_X2F16) { TVR_SKR(E, ACT_X2F16); } else { TVR_SKR(E, ACT_BF16); }
+  switch (epi) {
+    case EPI_BIAS: TVR_SKR_F(EPI_BIAS); break;
+    case EPI_SPLIT_GELU_ACT: TVR_SKR_F(EPI_SPLIT_GELU_ACT); break;
+    default: TVR_SKR_F(EPI_RESID); break;
+  }
+#undef TVR_SKR_F
+#undef TVR_SKR
+  return TVR_OK;
+}
+
 // Launch shape of a planar GEMM on 256 CUs (gemm_pingpong_kernel, one block
-// per CU): fewer than 192 tiles -> split-K over the whole launch; otherwise,
-// when the last round would run partly empty, its tiles (the raster's last
-// ones) go to a second launch with split-K, ceil(T S / 256) / S rounds instead
-// of one, if the round time saved beats the partial tiles' HBM round trip.
+// per CU).  Fewer than 256 tiles: stream-K over the whole launch (every CU
+// gets the same share of the k-iterations) when the round it saves beats two
+// partial tile epilogues per block and the fix-up's HBM round trip (else
+// split-K when fewer than 192); otherwise, when the last round would run
+// partly empty, its tiles (the raster's last ones) go stream-K (or split-K)
+// over all CUs when that pays.  Costs in us (tools/gemm_split_probe
+// anatomy: ~2.2 us per x2f16 k-tile per block, ~15 us per partial segment's
+// prologue + epilogue, fix-up at ~4 TB/s over the partials).
 struct PpPlan {
   int ksplit = 1;    // whole launch
   int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
   int tail_split = 1;
+  int sk_base = -1;  // >= 0: tiles [0, sk_base) plain, the rest stream-K over sk_blocks blocks
+  int sk_blocks = 0;
 };
+bool sk_enabled() { return env_flag("TVR_STREAM_K"); }
 PpPlan plan_pp(int M, int N, int K, int a_fmt) {
   PpPlan p;
   const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_X2F16 ? 32 : 64);
+  const double kt_us = a_fmt == ACT_X2F16 ? 2.2 : 1.5, seg_us = 15.0, epi_us = 10.0;
+  // stream-K of `cnt` tiles over min(256, iterations) blocks vs one plain round
+  auto sk_us = [&](int cnt) {
+    const int G = (int)std::min<long long>(256, (long long)cnt * nkt);
+    return std::ceil((double)cnt * nkt / G) * kt_us + 2.0 * seg_us + (cnt + 2.0 * G) * 0.0655 + 5.0;
+  };
+  const double round_plain_us = nkt * kt_us + epi_us;
+  if (sk_enabled() && (long long)tiles * nkt >= 4LL * 256) {
+    const int rounds = (tiles + 255) / 256;
+    const int tb = tiles - 256 * (rounds - 1);  // tiles of the last (partly empty) round
+    if (tb < 256 && sk_us(tb) + 5.0 < round_plain_us) {
+      p.sk_base = tiles - tb;
+      p.sk_blocks = (int)std::min<long long>(256, (long long)tb * nkt);
+      return p;
+    }
+  }
   if (tiles < 192) {
     p.ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
     return p;
@@ -478,7 +544,11 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     } else {
       PpPlan plan;
       if (m && vec && epi != EPI_STATS) plan = plan_pp(M, N, K, a_fmt);
-      if (plan.ksplit > 1) {
+      if (plan.sk_base >= 0) {
+        if (plan.sk_base > 0) launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.sk_base, true, st);
+        TVR_TRY(launch_pp_sk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.sk_base,
+                             gemm_pingpong_grid(M, N) - plan.sk_base, plan.sk_blocks, m, st));
+      } else if (plan.ksplit > 1) {
         TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, gemm_pingpong_grid(M, N),
                                  plan.ksplit, m, st));
       } else if (plan.tail_base > 0) {
@@ -1335,11 +1405,13 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
   const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
   const size_t o_lg = cv.take<float>(final_scratch_floats(m, act_fmt(m), FC, topk, out_logits));
-  const size_t o_cap = capture_zsum ? cv.take<float>((size_t)CAP_GROUPS * d) : 0;
-  // fp32 hook_z of each prompt's last row for the capture when no trace slot
-  // receives it (the attention kernel writes that row only, at row s)
+  const int n_cap = capture_zsum ? L - start_layer : 0;  // layers captured (one reduction after the loop)
+  const size_t o_cap = capture_zsum ? cv.take<float>((size_t)n_cap * CAP_GROUPS * d) : 0;
+  // fp32 hook_z of each prompt's last row, every layer, for the capture when no
+  // trace slot receives it (the attention kernel writes that row only, at row s
+  // of the layer's slab)
   const bool zf_last = capture_zsum && !trace;
-  const size_t o_zf = zf_last ? cv.take<float>((size_t)n_seq * d) : 0;
+  const size_t o_zf = zf_last ? cv.take<float>((size_t)n_cap * n_seq * d) : 0;
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -1373,7 +1445,8 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
                              hipMemcpyDeviceToDevice, st));
     float* qkv = trace ? trace->qkv + (size_t)l * 3 * tstride : a.qkv;
     // attention writes the fp32 hook_z straight into the trace (or the capture buffer)
-    float* zf = trace ? trace->z + l * tstride : (capture_zsum ? (float*)(base + o_zf) : nullptr);
+    float* zf = trace ? trace->z + l * tstride
+                      : (capture_zsum ? (float*)(base + o_zf) + (size_t)(l - start_layer) * n_seq * d : nullptr);
     const bool want_out = out_prob || out_topk || out_logits;
     if (trim && l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, R, (const SeqDesc*)(base + o_seqs_last), n_seq, maxT, a, nullptr,
@@ -1381,17 +1454,18 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
     } else {
       TVR_TRY(run_block(m, l, R, d_seqs, n_seq, maxT, a, qkv, nullptr, zf, st, zf_last));
     }
-    if (capture_zsum) {
-      float* part = (float*)(base + o_cap);
-      ProfSpan ps(m, st);
-      hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS), dim3(64), 0, st,
-                         zf, d, zf_last ? nullptr : d_last, n_seq, part, d);
-      hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part,
-                         capture_zsum + (size_t)l * d, d);
-      TVR_HIP(hipGetLastError());
-      ps.done(TVR_HBM_CAPTURE, ((double)n_seq + 1.0) * d * 4.0);  // hook_z at every last row in, [d] out
-    }
     if (!(trim && l == L - 1)) TVR_TRY(run_block_out(m, l, R, a, st));
+  }
+  if (capture_zsum) {  // every layer's Σ over prompts of hook_z at the last row: one launch pair
+    float* part = (float*)(base + o_cap);
+    const float* z0 = trace ? trace->z + start_layer * tstride : (const float*)(base + o_zf);
+    ProfSpan ps(m, st);
+    hipLaunchKernelGGL(capture_partial_kernel, dim3((d / 4 + 63) / 64, CAP_GROUPS, n_cap), dim3(64), 0, st,
+                       z0, d, trace ? tstride : (size_t)n_seq * d, zf_last ? nullptr : d_last, n_seq, part, d);
+    hipLaunchKernelGGL(capture_finish_kernel, dim3((d + 255) / 256, n_cap), dim3(256), 0, st, part,
+                       capture_zsum + (size_t)start_layer * d, d);
+    TVR_HIP(hipGetLastError());
+    ps.done(TVR_HBM_CAPTURE, (double)n_cap * ((double)n_seq + 1.0) * d * 4.0);  // hook_z at every last row in, [L][d] out
   }
   if (trace) {
     TVR_HIP(hipMemcpyAsync(trace->resid + L * tstride, a.resid, (size_t)R * d * sizeof(float),

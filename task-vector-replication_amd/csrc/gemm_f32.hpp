@@ -85,6 +85,14 @@ struct GemmEpi {
   int tile_base;
   int tile_count;
   int group_m;  // gemm_pingpong_kernel raster: m-blocks per group (0: GEMM_GROUP_M)
+  // Stream-K (gemm_pingpong_kernel, sk_blocks > 0; EPI_BIAS, bias nullptr):
+  // sk_blocks blocks share the tile_count x (K / BK) k-iterations of tiles
+  // [tile_base, tile_base + tile_count) evenly, block g taking iterations
+  // [g I / G, (g + 1) I / G) (at most two tile segments: sk_blocks >=
+  // tile_count); segment j of block g stores its fp32 partial tile at
+  // out0 + (2 g + j) * 256 * 256, which splitk_sk_reduce_kernel sums per tile
+  // in k order under the real epilogue.
+  int sk_blocks;
   // EPI_STATS: record of (row m, column tile t) at stats + (m * stats_tiles + t) * (2 + 2 stats_k):
   // {max, sum exp, value[stats_k], column[stats_k] (int bits)}; targets[m] (may be null) selects
   // the logit written to tlogit[m].

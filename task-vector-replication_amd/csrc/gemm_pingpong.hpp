@@ -252,39 +252,35 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
 // same instruction stream: timing only).
-template <int EPI, int FMT, bool VEC = true, int VAR = 0>
-__global__ void __launch_bounds__(PP_THREADS, 1)
-gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
-                     size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
+// LDS of one block: 2 stages x (A, W) planes + a 1 KB staging sink, or the
+// epilogue's 128-row half, whichever is larger
+template <int FMT>
+struct PpLds {
+  using F = PlanarFmt<FMT>;
+  static constexpr int BUF = 2 * F::NPL * 256 * F::BK;
+  static constexpr int HALVES = (2 * BUF + 512) > PP_EPI_LDS ? (2 * BUF + 512) : PP_EPI_LDS;
+};
+
+// One output tile (m0, n0) over k-tiles [kbeg, kbeg + nk) of this block:
+// prologue, the phase-split K loop, epilogue.  part != nullptr: the fp32
+// partial tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256
+// tile (split-K / stream-K), else the launch's fused epilogue.
+template <int EPI, int FMT, bool VEC, int VAR>
+__device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda, size_t aps,
+                                        const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale, int M,
+                                        int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part,
+                                        uint16_t* lds, unsigned long long st0, unsigned long long sr0) {
   using F = PlanarFmt<FMT>;
   using frag = typename F::frag;
-  const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;  // clock diagnostics
-  const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   constexpr int NPL = F::NPL, BK = F::BK, KG = BK / 32;
   constexpr int CPR = BK / 8;          // 16-B chunks per plane row
   constexpr int RPP = 64 / CPR;        // rows per 1 KB piece
   constexpr int PPP = 128 / RPP;       // pieces per plane per region (128 rows)
   constexpr int PL = 256 * BK;         // halves per plane per buffer
-  constexpr int BUF = 2 * NPL * PL;    // halves per buffer: A planes, then W planes
+  constexpr int BUF = PpLds<FMT>::BUF; // halves per buffer: A planes, then W planes
   constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
   static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
-  constexpr int LDS_HALVES = (2 * BUF + 512) > PP_EPI_LDS ? (2 * BUF + 512) : PP_EPI_LDS;
-  static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
-  // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_HALVES];
-
-  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
-  // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
-  // each split over S k-ranges (block = (tile, split))
-  const int S = ep.k_split > 1 ? ep.k_split : 1;
-  const int count = ep.tile_count > 0 ? ep.tile_count : nbm * nbn;
-  const int nwg = count * S;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgs = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int lt = wgs / S, split = wgs - lt * S;
-  int m0, n0;
-  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M);
+  static_assert(PpLds<FMT>::HALVES * 2 <= 160 * 1024, "LDS budget");
 
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
@@ -316,9 +312,6 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       }
     }
   }
-  const int nk_all = K / BK;
-  const int kbeg = (int)((long long)split * nk_all / S);
-  const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
   auto stage = [&](int R, int kt) {
     if (VAR == 1 && kt >= 2) return;
     const bool live = kt < nk;
@@ -453,9 +446,9 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
   if constexpr (VEC && VAR != 7) {  // epilogue through LDS (VAR 7: the register epilogue, for A/B)
     __syncthreads();  // every wave's DMA retired (vmcnt(0) above) and last LDS reads done
     float* L = reinterpret_cast<float*>(lds);
-    if (S > 1) {
+    if (part) {
       GemmEpi pe = ep;
-      pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
+      pe.out0 = part;
       pe.ld0 = 256;
       pe.out_rows = nullptr;  // partial tiles are stored densely; the reduce applies out_rows
       pp_epilogue_lds<EPI, FMT, VAR == 8>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
@@ -480,9 +473,9 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
     }
-    if (S > 1) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
+    if (part) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
       GemmEpi pe = ep;
-      pe.out0 = ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS;
+      pe.out0 = part;
       pe.ld0 = 256;
       gemm_epilogue16t<EPI, FMT, VEC, 8, 4>(pe, acc, M - m0, N - n0, wr * 128, wc * 64, lane);
     } else {
@@ -499,6 +492,63 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
     }
   }
+}
+
+// K must be a multiple of BK (host-checked); any M, N.
+// VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
+// (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
+// waits in the loop (racy: timing only), 6 per-block stamps (start, loop
+// start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
+// epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
+// skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
+// same instruction stream: timing only).
+template <int EPI, int FMT, bool VEC = true, int VAR = 0>
+__global__ void __launch_bounds__(PP_THREADS, 1)
+gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
+                     size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
+  const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;  // clock diagnostics
+  const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[PpLds<FMT>::HALVES];
+  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
+  const int nk_all = K / PlanarFmt<FMT>::BK;
+  const int gm = ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M;
+  // XCD-aware bijective remap: the blocks of one XCD (b = x mod 8) take a
+  // contiguous range of logical indices, so neighbouring tiles (and a
+  // stream-K tile's consecutive contributors) share that XCD's L2
+  auto remap = [](int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  };
+  if (ep.sk_blocks > 0) {  // stream-K: this block's even share of the launch's k-iterations
+    const int G = ep.sk_blocks, count = ep.tile_count;
+    const int g = remap(blockIdx.x, G);
+    const long long I = (long long)count * nk_all;
+    long long it = (long long)g * I / G;
+    const long long it1 = (long long)(g + 1) * I / G;
+    for (int seg = 0; it < it1 && seg < 2; ++seg) {
+      const int lt = (int)(it / nk_all), k0 = (int)(it - (long long)lt * nk_all);
+      const int nk = (int)min((long long)(nk_all - k0), it1 - it);
+      int m0, n0;
+      pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
+      pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, k0, nk,
+                                  ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, lds, st0, sr0);
+      it += nk;
+    }
+    return;
+  }
+  // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
+  // each split over S k-ranges (block = (tile, split))
+  const int S = ep.k_split > 1 ? ep.k_split : 1;
+  const int count = ep.tile_count > 0 ? ep.tile_count : nbm * nbn;
+  const int wgs = remap(blockIdx.x, count * S);
+  const int lt = wgs / S, split = wgs - lt * S;
+  int m0, n0;
+  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
+  const int kbeg = (int)((long long)split * nk_all / S);
+  const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
+  pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+                              S > 1 ? ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS : nullptr, lds, st0, sr0);
 }
 
 // Sum of the k_split partial tiles [S][count][256][256] (fixed order:
@@ -519,6 +569,41 @@ splitk_reduce_kernel(const float* __restrict__ part, int S, int tile_base, int c
     const float* p = part + (size_t)lt * PP_TILE_ELEMS + e;
     f32x4 v = *(const f32x4*)p;
     for (int s = 1; s < S; ++s) v += *(const f32x4*)(p + (size_t)s * count * PP_TILE_ELEMS);
+    if (ep.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += ep.bias[c + r];
+    }
+    const size_t orow = ep.out_rows ? (size_t)ep.out_rows[m] : (size_t)m;
+    epi_store4<EPI, FMT>(ep, orow, c, v);
+  }
+}
+
+// Stream-K fix-up: tile lt's k-iterations [lt KT, (lt + 1) KT) were covered by
+// the blocks g = b0 .. b1 (block g holds [floor(g I / G), floor((g + 1) I / G)),
+// so the block holding iteration x is floor(((x + 1) G - 1) / I)); each left
+// its share in slot 1 if it began in an earlier tile, else slot 0.  Summed in
+// block (= k) order: deterministic.  Then bias + the launch's epilogue, four
+// consecutive columns per thread (host-checked as splitk_reduce_kernel).
+template <int EPI, int FMT>
+__global__ void __launch_bounds__(256)
+splitk_sk_reduce_kernel(const float* __restrict__ part, int G, int KT, int tile_base, int count, int M, int N,
+                        GemmEpi ep) {
+  const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
+  const long long I = (long long)count * KT;
+  const size_t total = (size_t)count * (PP_TILE_ELEMS / 4);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int lt = (int)(i / (PP_TILE_ELEMS / 4)), e = (int)(i % (PP_TILE_ELEMS / 4)) * 4;
+    int m0, n0;
+    pp_tile_coords(tile_base + lt, nbm, nbn, m0, n0, ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M);
+    const int m = m0 + (e >> 8), c = n0 + (e & 255);
+    if (m >= M || c >= N) continue;
+    const long long x0 = (long long)lt * KT, x1 = x0 + KT - 1;
+    const int b0 = (int)(((x0 + 1) * G - 1) / I), b1 = (int)(((x1 + 1) * G - 1) / I);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int b = b0; b <= b1; ++b) {
+      const int slot = ((long long)b * I / G) < x0 ? 1 : 0;
+      v += *(const f32x4*)(part + ((size_t)2 * b + slot) * PP_TILE_ELEMS + e);
+    }
     if (ep.bias) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += ep.bias[c + r];

@@ -237,16 +237,19 @@ entry_kernel(const EntryDesc* __restrict__ ents, const float* __restrict__ snap,
 
 // ---------------------------------------------------------------------------
 // Capture + mean-over-prompts reduction, z form (mean_p result =
-// (mean_p z) @ W_O).  Deterministic two-pass: partial[g][c] = sum over rows
-// g, g+G, ...; then zsum[c] += sum_g partial[g][c].  rows == nullptr: row i is
-// z row i (the attention kernel's compact last-row copy).
+// (mean_p z) @ W_O), for every layer of a forward in ONE pair of launches
+// after the layer loop (blockIdx.z = layer; layer l's hook_z rows at
+// z + l * zstride).  Deterministic two-pass: partial[l][g][c] = sum over rows
+// g, g+G, ...; then zsum[l][c] += sum_g partial[l][g][c].  rows == nullptr:
+// row i is z row i (the attention kernel's compact last-row copy).
 constexpr int CAP_GROUPS = 128;  // row groups of the partial pass (fixed-order sums: deterministic)
-__global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
+__global__ void capture_partial_kernel(const float* __restrict__ z, int ldz, size_t zstride,
                                        const int32_t* __restrict__ rows, int n,
                                        float* __restrict__ partial, int d) {
   const int c4 = blockIdx.x * blockDim.x + threadIdx.x;  // float4 column
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, l = blockIdx.z;
   if (c4 * 4 >= d) return;
+  z += (size_t)l * zstride;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   int i = g;
   for (; i + 3 * CAP_GROUPS < n; i += 4 * CAP_GROUPS) {  // four rows' loads in flight, summed in row order
@@ -265,15 +268,17 @@ __global__ void capture_partial_kernel(const float* __restrict__ z, int ldz,
     const float4 v = ((const float4*)(z + (size_t)(rows ? rows[i] : i) * ldz))[c4];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
-  ((float4*)(partial + (size_t)g * d))[c4] = s;
+  ((float4*)(partial + ((size_t)l * CAP_GROUPS + g) * d))[c4] = s;
 }
+
 __global__ void capture_finish_kernel(const float* __restrict__ partial,
                                       float* __restrict__ zsum, int d) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, l = blockIdx.y;
   if (c >= d) return;
+  partial += (size_t)l * CAP_GROUPS * d;
   float s = 0.f;
   for (int g = 0; g < CAP_GROUPS; ++g) s += partial[(size_t)g * d + c];
-  zsum[c] += s;
+  zsum[(size_t)l * d + c] += s;
 }
 
 // out[l][h][c] = sum_k zsum[l][h*dh + k] * w2_l[c][h*dh + k]

@@ -17,8 +17,8 @@
 // raises ValueError (the reference's shape errors, scratch2.py:172-175),
 // everything else RuntimeError.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <string>
@@ -40,7 +40,11 @@ tvr_model* as_model(int64_t h) {
   return reinterpret_cast<tvr_model*>(static_cast<intptr_t>(h));
 }
 
-void* cur_stream(const c10::Device& dev) { return c10::hip::getCurrentHIPStream(dev.index()).stream(); }
+// torch's ROCm build presents HIP devices as DeviceType::CUDA: its guard and
+// current-stream accessors are the "masquerading" ones
+using DeviceGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
+
+void* cur_stream(const c10::Device& dev) { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev.index()).stream(); }
 
 void need_gpu(const c10::Device& dev) {
   TORCH_CHECK(dev.is_cuda(), "the HIP engine needs a GPU device (no CPU fallback): got device ", dev);
@@ -75,7 +79,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> forward_clean(
   const int64_t n = seq_lens.numel();
   TORCH_CHECK_VALUE(n > 0, "tvr: no prompts");
   need_gpu(device);
-  c10::hip::HIPGuard guard(device);
+  DeviceGuard guard(device);
   const int32_t* tg = opt_host_i32(targets, "targets");
   TORCH_CHECK_VALUE(!targets.has_value() || targets->numel() == n, "targets must have one entry per prompt");
   auto prob = tg ? at::empty({n}, f32(device)) : at::empty({0}, f32(device));
@@ -112,7 +116,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> patch_sweep(int64_t model, int64_
   TORCH_CHECK_VALUE(n > 0, "tvr: no patch sites");
   TORCH_CHECK_VALUE(trace != 0, "tvr: patch_sweep needs a trace");
   need_gpu(device);
-  c10::hip::HIPGuard guard(device);
+  DeviceGuard guard(device);
   const float* vec = in_f32(vectors, device, "vectors");
   const int32_t nvec = vectors.has_value() ? (int32_t)(vectors->numel() / std::max<int64_t>(vectors->size(-1), 1)) : 0;
   auto prob = want_prob ? at::empty({n}, f32(device)) : at::empty({0}, f32(device));
@@ -131,7 +135,7 @@ at::Tensor project_heads(int64_t model, const at::Tensor& zsum, int64_t n_heads)
   TORCH_CHECK_VALUE(zsum.dim() == 2, "tvr: zsum must be [n_layers, d_model]");
   const c10::Device dev = zsum.device();
   need_gpu(dev);
-  c10::hip::HIPGuard guard(dev);
+  DeviceGuard guard(dev);
   const float* z = in_f32(zsum, dev, "zsum");
   auto out = at::empty({zsum.size(0), n_heads, zsum.size(1)}, f32(dev));
   check(tvr_project_heads(as_model(model), z, out.data_ptr<float>(), cur_stream(dev)), "tvr_project_heads");
@@ -144,7 +148,7 @@ at::Tensor forward_logits(int64_t model, const std::optional<at::Tensor>& tokens
                           const std::optional<at::Tensor>& resid, int64_t start_layer, const at::Tensor& seq_lens,
                           int64_t d_vocab, c10::Device device) {
   need_gpu(device);
-  c10::hip::HIPGuard guard(device);
+  DeviceGuard guard(device);
   const int32_t* lens = host_i32(seq_lens, "seq_lens");
   int64_t rows = 0;
   for (int64_t i = 0; i < seq_lens.numel(); ++i) rows += lens[i];

@@ -1,0 +1,52 @@
+"""Stream-K GEMM launches (csrc/gemm_pingpong.hpp ``sk_blocks``,
+splitk_sk_reduce_kernel; engine.hip plan_pp) against the plain / split-K
+launches (``TVR_STREAM_K=0``), on the small-M shapes they serve: the C2
+layer sweeps (52 prompts x T0 = 3: M = 156 + 52 l rows, 70 column tiles of
+the QKV + MLP-in GEMM, 10 of the O + MLP-out one) and a CIE sweep, at the
+Pythia-2.8B width (3 layers, std-0.1 weights so the outputs are
+informative).  The two differ only in fp32 summation order: logits within
+1e-5 relative, probabilities / CIE within 1e-4 of the largest + 1e-7,
+top-1 identical; both against the fp32 CPU oracle at the same bars."""
+import pytest
+import torch
+
+import tvr_amd
+from conftest import make_oracle
+from oracle import reference_experiments as R
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+@pytest.mark.timeout(900)
+def test_stream_k_matches_plain_launches(monkeypatch):
+    cfg = tvr_amd.get_config("pythia-2.8b").with_(n_layers=3)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok)
+    oracle = make_oracle(cfg, sd, tok)
+    task = list(tvr_amd.tasks.letter_to_caps)
+    arrow = tvr_amd.tasks.ARROW
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 2, 4, seed=1234)
+    answers = [int(t) for t in model.forward_clean(prompts, topk=1)["topk"][:, 0].tolist()]
+    g = torch.Generator().manual_seed(5)
+    mean = (torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5).cuda()
+    layered = tvr_amd.gather_head_activations_to_layers(mean)
+    out = {}
+    for sk in ("1", "0"):
+        monkeypatch.setenv("TVR_STREAM_K", sk)
+        clean = model.forward_clean([[0, 5, 9]] * 52, topk=1, return_logits=True)  # 156 rows: 70 + 10 tiles
+        dp = tvr_amd.apply_layered_vectors_to_zero_shot_by_probability(layered, task, arrow, model=model)
+        acc = tvr_amd.apply_layered_vectors_to_zero_shot(layered, task, arrow, model=model)
+        cie = tvr_amd.experiments.causal_indirect_effect_sums(mean, prompts, answers, model).cpu().double()
+        out[sk] = (clean["logits"][0].cpu().double(), dp.cpu().double(), acc, cie)
+    (l1, d1, a1, c1), (l0, d0, a0, c0) = out["1"], out["0"]
+    assert ((l1 - l0).abs().max() / l0.abs().max()).item() < 1e-5
+    assert (d1 - d0).abs().max().item() <= 1e-4 * d0.abs().max().item() + 1e-7
+    assert a1 == a0
+    assert (c1 - c0).abs().max().item() <= 1e-4 * c0.abs().max().item() + 1e-7
+    # both against the CPU oracle (the reference's loops)
+    ref = oracle.forward(torch.tensor([[0, 5, 9]]))[0, -1].double()
+    assert ((l1 - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    ref_dp = R.apply_layered_vectors_to_zero_shot_by_probability(layered.cpu(), task, arrow, oracle).double()
+    assert (d1 - ref_dp).abs().max().item() <= 1e-4 * ref_dp.abs().max().item() + 1e-7
+    model._check_range("stream-K test")
