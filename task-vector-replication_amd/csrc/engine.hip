@@ -400,13 +400,13 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
   pe.tile_count = count;
   const dim3 g(G), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
   if (a_fmt == ACT_X2F16)
-    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_F16)
-    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_F16, true, 0, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else
-    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 0, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   const int KT = K / (a_fmt == ACT_X2F16 ? 32 : 64);
 #define TVR_SKR(E, F)                                                                                         \

@@ -262,14 +262,15 @@ struct PpLds {
 };
 
 // One output tile (m0, n0) over k-tiles [kbeg, kbeg + nk) of this block:
-// prologue, the phase-split K loop, epilogue.  part != nullptr: the fp32
-// partial tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256
-// tile (split-K / stream-K), else the launch's fused epilogue.
+// prologue, the phase-split K loop, epilogue.  has_part: the fp32 partial
+// tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256 tile
+// (split-K / stream-K), else the launch's fused epilogue.  (A separate int
+// flag: testing the pointer itself made hipcc spill 26-66 VGPRs.)
 template <int EPI, int FMT, bool VEC, int VAR>
 __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda, size_t aps,
                                         const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale, int M,
-                                        int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part,
-                                        uint16_t* lds, unsigned long long st0, unsigned long long sr0) {
+                                        int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part, int has_part,
+                                        unsigned long long st0, unsigned long long sr0) {
   using F = PlanarFmt<FMT>;
   using frag = typename F::frag;
   constexpr int NPL = F::NPL, BK = F::BK, KG = BK / 32;
@@ -281,8 +282,16 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
   static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
   static_assert(PpLds<FMT>::HALVES * 2 <= 160 * 1024, "LDS budget");
+  // ONE __shared__ object (a second one can make hipcc drain vmcnt before
+  // ds_reads), declared here so every access is a known LDS address (a
+  // generic pointer parameter costs VGPRs: 64-bit flat addresses)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[PpLds<FMT>::HALVES];
 
-  const int t = threadIdx.x;
+  // the thread index through an empty asm: a stream-K block's two inlined
+  // tiles then recompute their lane addresses instead of one copy holding the
+  // other's live across its K loop (VGPR spills)
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
   const int wave = t >> 6, lane = t & 63;
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -446,7 +455,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   if constexpr (VEC && VAR != 7) {  // epilogue through LDS (VAR 7: the register epilogue, for A/B)
     __syncthreads();  // every wave's DMA retired (vmcnt(0) above) and last LDS reads done
     float* L = reinterpret_cast<float*>(lds);
-    if (part) {
+    if (has_part) {
       GemmEpi pe = ep;
       pe.out0 = part;
       pe.ld0 = 256;
@@ -473,7 +482,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] *= acc_scale;
     }
-    if (part) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
+    if (has_part) {  // partial product of (split, tile) as a 256 x 256 fp32 tile (EPI_BIAS launches; host-checked)
       GemmEpi pe = ep;
       pe.out0 = part;
       pe.ld0 = 256;
@@ -501,15 +510,14 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
-// same instruction stream: timing only).
-template <int EPI, int FMT, bool VEC = true, int VAR = 0>
+// same instruction stream: timing only).  SKM: the stream-K form (sk_blocks
+// blocks; EPI_BIAS partial tiles only).
+template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
                      size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
   const unsigned long long st0 = ep.stamps ? __builtin_amdgcn_s_memtime() : 0;  // clock diagnostics
   const unsigned long long sr0 = ep.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  // ONE __shared__ object (a second one can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[PpLds<FMT>::HALVES];
   const int nbm = (M + 255) >> 8, nbn = (N + 255) >> 8;
   const int nk_all = K / PlanarFmt<FMT>::BK;
   const int gm = ep.group_m > 0 ? ep.group_m : GEMM_GROUP_M;
@@ -520,35 +528,44 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   };
-  if (ep.sk_blocks > 0) {  // stream-K: this block's even share of the launch's k-iterations
-    const int G = ep.sk_blocks, count = ep.tile_count;
+  const int count = ep.tile_count > 0 ? ep.tile_count : nbm * nbn;
+  if constexpr (SKM) {
+    // stream-K: block g takes the k-iterations [g I / G, (g + 1) I / G) of
+    // the launch's tiles, at most two segments (G >= tiles).  A template of its
+    // own: the segment loop around the K loop costs VGPRs the plain launches
+    // (one segment, no loop) must not pay.
+    const int G = ep.sk_blocks;
     const int g = remap(blockIdx.x, G);
     const long long I = (long long)count * nk_all;
     long long it = (long long)g * I / G;
     const long long it1 = (long long)(g + 1) * I / G;
-    for (int seg = 0; it < it1 && seg < 2; ++seg) {
-      const int lt = (int)(it / nk_all), k0 = (int)(it - (long long)lt * nk_all);
-      const int nk = (int)min((long long)(nk_all - k0), it1 - it);
+    // the (at most) two segments as straight-line code: a loop around the
+    // K loop kept its state live across iterations (68-83 VGPRs spilled)
+    auto segment = [&](int seg) {
+      const int lt = (int)(it / nk_all);
+      const int kbeg = (int)(it - (long long)lt * nk_all);
+      const int nk = (int)min((long long)(nk_all - kbeg), it1 - it);
       int m0, n0;
       pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-      pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, k0, nk,
-                                  ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, lds, st0, sr0);
+      pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+                                  ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, 1, st0, sr0);
       it += nk;
-    }
-    return;
+    };
+    segment(0);
+    if (it < it1) segment(1);
+  } else {
+    // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
+    // each split over S k-ranges (block = (tile, split))
+    const int S = ep.k_split > 1 ? ep.k_split : 1;
+    const int wgs = remap(blockIdx.x, count * S);
+    const int lt = wgs / S, split = wgs - lt * S;
+    int m0, n0;
+    pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
+    const int kbeg = (int)((long long)split * nk_all / S);
+    const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
+    pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+                                ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS, S > 1, st0, sr0);
   }
-  // this launch: tiles [tile_base, tile_base + count) of the grouped raster,
-  // each split over S k-ranges (block = (tile, split))
-  const int S = ep.k_split > 1 ? ep.k_split : 1;
-  const int count = ep.tile_count > 0 ? ep.tile_count : nbm * nbn;
-  const int wgs = remap(blockIdx.x, count * S);
-  const int lt = wgs / S, split = wgs - lt * S;
-  int m0, n0;
-  pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-  const int kbeg = (int)((long long)split * nk_all / S);
-  const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
-  pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
-                              S > 1 ? ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS : nullptr, lds, st0, sr0);
 }
 
 // Sum of the k_split partial tiles [S][count][256][256] (fixed order:
