@@ -285,3 +285,120 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
 }
 
 }  // namespace tvr
+
+namespace tvr {
+
+// Single-query attention (the patched forwards of last-position sites:
+// ADD_ATTN_OUT_LASTPOS / NONE, one computed row per sequence, q0 = n - 1 —
+// the C2 layer sweeps, FV evaluations and head-count grid): a 16-query MFMA
+// tile per (sequence, head) wastes 15 of its 16 rows there.  Here ONE wave
+// serves HG heads of one sequence: lane l holds E = HG DH / 64 consecutive
+// dims (head l / (DH / E), chunk l mod (DH / E)), so the query / key / value
+// slices of the wave's heads are one contiguous, coalesced load per row; the
+// head's q.k is a butterfly over its DH / E lanes, the softmax is online over
+// the keys (fp32, the same -inf-free form: every key <= the query), and z goes
+// out as one contiguous span per wave.  Rotary (TL rotate-half on dims
+// [0, DH / 4)): the partner of dim i (i +- rd / 2) sits in lane l ^ (rd / 2 / E)
+// at the same element (E divides rd / 2 for every Pythia head size).
+template <int DH>
+struct RowAttnShape {
+  static constexpr int HG = DH == 128 ? 2 : 4;  // heads per wave
+  static constexpr int E = HG * DH / 64;        // dims per lane (16: 1, 64: 4, 80: 5, 128: 4)
+  static constexpr int LPH = DH / E;            // lanes per head
+};
+
+template <int FMT, int DH>
+__global__ void __launch_bounds__(256)
+attention_row_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
+                     const SeqDesc* __restrict__ seqs, int s_begin, int n_seqs, int n_heads, void* __restrict__ z,
+                     int ldz, float* __restrict__ zf, int ldzf, int zf_last, int zf_rows, unsigned* __restrict__ flag,
+                     const float* __restrict__ cos_t, const float* __restrict__ sin_t, int d, float inv_attn_scale) {
+  using S = RowAttnShape<DH>;
+  constexpr int E = S::E, LPH = S::LPH, HG = S::HG;
+  constexpr int rd = DH / 4, half = rd / 2, OFF = half / E;  // partner lane distance (xor)
+  static_assert(half % E == 0 && (OFF & (OFF - 1)) == 0, "rotary pairs must map onto lane pairs");
+  const int lane = threadIdx.x & 63;
+  const int groups = n_heads / HG;
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= n_seqs * groups) return;  // a whole wave
+  const int s = s_begin + wid / groups, h0 = (wid % groups) * HG;
+  const SeqDesc sd = seqs[s];
+  const int T = sd.p0 + sd.n, qpos = T - 1;
+  const int e = lane % LPH;                 // chunk of the head
+  const int col = h0 * DH + lane * E;       // this lane's first column within a Q / K / V block
+  const float* pfx = sd.prefix_live ? qkv : cache;
+  const int ldp = sd.prefix_live ? ldq : ldc;
+  auto row_of = [&](int j) -> const float* {
+    return j < sd.p0 ? pfx + (size_t)(sd.cache_row + j) * ldp : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
+  };
+  auto rotate = [&](float (&x)[E], int pos) {
+    float p[E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) p[i] = __shfl_xor(x[i], OFF, 64);  // every lane, before any divergence
+    if (e < 2 * OFF) {
+      const float sg = (e & OFF) == 0 ? -1.f : 1.f;  // x0 cos - x1 sin | x1 cos + x0 sin
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        const int dim = e * E + i;
+        x[i] = x[i] * cos_t[pos * rd + dim] + sg * p[i] * sin_t[pos * rd + dim];
+      }
+    }
+  };
+  float q[E];
+  {
+    const float* r = row_of(qpos) + col;
+#pragma unroll
+    for (int i = 0; i < E; ++i) q[i] = r[i];
+    rotate(q, qpos);
+  }
+  float m_run = -INFINITY, l_run = 0.f, acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  constexpr int KB = 4;  // keys per batch: their loads in flight together
+  for (int j0 = 0; j0 < T; j0 += KB) {
+    float kv[KB][E], vv[KB][E];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int j = min(j0 + u, T - 1);
+      const float* r = row_of(j);
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        kv[u][i] = r[d + col + i];
+        vv[u][i] = r[2 * d + col + i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int j = j0 + u;
+      rotate(kv[u], min(j, T - 1));
+      float sc = 0.f;
+#pragma unroll
+      for (int i = 0; i < E; ++i) sc = fmaf(q[i], kv[u][i], sc);
+#pragma unroll
+      for (int o = LPH / 2; o > 0; o >>= 1) sc += __shfl_xor(sc, o, 64);
+      if (j >= T) continue;  // wave-uniform (T is the sequence's)
+      sc *= inv_attn_scale;
+      const float m_new = fmaxf(m_run, sc);
+      const float scale = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+      const float p = expf(sc - m_new);
+      l_run = l_run * scale + p;
+#pragma unroll
+      for (int i = 0; i < E; ++i) acc[i] = fmaf(p, vv[u][i], acc[i] * scale);
+      m_run = m_new;
+    }
+  }
+  const size_t zrow = (size_t)(sd.row0 + sd.n - 1);
+  const float inv = 1.0f / l_run;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const float v = acc[i] * inv;
+    if constexpr (FMT != ACT_F32)
+      store_act<FMT>((uint16_t*)z + zrow * 2 * ldz + col + i, ldz, v, flag);
+    else
+      ((float*)z)[zrow * ldz + col + i] = v;
+    if (zf && zf_last) zf[(size_t)s * ldzf + col + i] = v;  // the capture's compact last-row copy
+    else if (zf && zrow < (size_t)zf_rows) zf[zrow * ldzf + col + i] = v;
+  }
+}
+
+}  // namespace tvr

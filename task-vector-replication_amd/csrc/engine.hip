@@ -732,14 +732,44 @@ struct Acts {
 // attention_mfma_kernel (one wave per (sequence, head), fp32 MFMA, no LDS) for
 // the Pythia head sizes d_head 16 (tiny), 64, 80, 128 with rotary_dim =
 // d_head / 4 (every Pythia: rotary_pct 0.25); check_config rejects the rest.
+// row_from: sequences [row_from, n_seqs) have exactly one query row (their
+// last: q0 = n - 1) and go to attention_row_kernel (HG heads per wave).
+bool row_attention_ok(const tvr_config& c) {
+  const int hg = c.d_head == 128 ? 2 : 4;
+  return c.n_heads % hg == 0 && (c.d_head == 16 || c.d_head == 64 || c.d_head == 80 || c.d_head == 128);
+}
+
 int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, const SeqDesc* d_seqs,
                      int n_seqs, int maxT, void* z, int fmt, float* zf, hipStream_t st, bool zf_last = false,
-                     int zf_rows = INT_MAX) {
+                     int zf_rows = INT_MAX, int row_from = INT_MAX) {
   if (n_seqs <= 0) return TVR_OK;
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const float inv_scale = 1.0f / std::sqrt((float)c.d_head);
   const int dh = c.d_head;
+  if (row_from < n_seqs && row_attention_ok(c) && env_flag("TVR_ROW_ATTN")) {  // TVR_ROW_ATTN=0: A/B, tests
+    const int nr = n_seqs - row_from, hg = dh == 128 ? 2 : 4;
+    const dim3 rg((nr * (c.n_heads / hg) + 3) / 4), rb(256);
+#define TVR_ATTR(F, DHV)                                                                                         \
+  hipLaunchKernelGGL((attention_row_kernel<F, DHV>), rg, rb, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, row_from, \
+                     nr, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, \
+                     d, inv_scale)
+#define TVR_ATTR_DH(F)                                                                         \
+  if (dh == 16) { TVR_ATTR(F, 16); } else if (dh == 64) { TVR_ATTR(F, 64); }                   \
+  else if (dh == 80) { TVR_ATTR(F, 80); } else { TVR_ATTR(F, 128); }
+    if (fmt == ACT_X2F16) {
+      TVR_ATTR_DH(ACT_X2F16);
+    } else if (fmt == ACT_BF16) {
+      TVR_ATTR_DH(ACT_BF16);
+    } else {
+      TVR_ATTR_DH(ACT_F32);
+    }
+#undef TVR_ATTR_DH
+#undef TVR_ATTR
+    TVR_HIP(hipGetLastError());
+    n_seqs = row_from;  // the MFMA kernel takes the rest (below)
+    if (n_seqs <= 0) return TVR_OK;
+  }
   const int pairs = n_seqs * c.n_heads;
   const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
   // key tiles in registers: 1 / 2 / 4 / 8, or 0 = longer than 128 (chunked online softmax)
@@ -838,7 +868,7 @@ int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const G
 // zf_last: the fp32 hook_z copy of each sequence's last row only, at row s of zf
 int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT,
               Acts& a, float* qkv_out, const float* cache_qkv, float* zf, hipStream_t st, bool zf_last = false,
-              int zf_rows = INT_MAX) {
+              int zf_rows = INT_MAX, int row_from = INT_MAX) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -846,7 +876,8 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
   TVR_TRY(launch_w1(m, l, a.xn, R, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
+  TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows,
+                           row_from));
   ps.done(TVR_HBM_ATTENTION, attention_bytes(d, R, R, a.fmt, zf ? (zf_last ? n_seqs : std::min(R, zf_rows)) : 0));
   return TVR_OK;
 }
@@ -875,7 +906,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e1.out_rows = d_last;
   TVR_TRY(launch_w1(m, l, a.xn, n_last, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows));
+  // every sequence queries its last row only (d_seqs carries q0 = n - 1): the single-query kernel
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows, 0));
   ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? std::min(n_last, zf_rows) : 0));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
@@ -1612,6 +1644,11 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
         return fail(TVR_ERR_INVALID, "site " + std::to_string(i) + ": unknown kind");
     }
   }
+  // every site computes one row (its last position: ADD_ATTN_OUT_LASTPOS,
+  // NONE, a SET_RESID_PRE_POS of the last position): the site sequences go to
+  // the single-query attention kernel
+  bool single_rows = true;
+  for (int i = 0; i < n_sites; ++i) single_rows = single_rows && nrow[i] == 1;
   // Shared prefixes (REPLACE_HEAD_ALLPOS): sites with the same (layer, head,
   // vector) whose sequences start with the same tokens compute identical rows
   // over that common prefix (position j attends to positions <= j only, and
@@ -1991,7 +2028,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
       TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), nc + cnt_le[l], maxT, a, cache,
                                   (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc));
     } else {
-      TVR_TRY(run_block(m, l, Rl, d_seqs, nc + cnt_le[l], maxT, a, a.qkv, cache, zf, st, false, Rc));
+      TVR_TRY(run_block(m, l, Rl, d_seqs, nc + cnt_le[l], maxT, a, a.qkv, cache, zf, st, false, Rc,
+                        single_rows ? nc : INT_MAX));
       TVR_TRY(run_block_out(m, l, Rl, a, st));
     }
     if (fused)

@@ -50,3 +50,44 @@ def test_stream_k_matches_plain_launches(monkeypatch):
     ref_dp = R.apply_layered_vectors_to_zero_shot_by_probability(layered.cpu(), task, arrow, oracle).double()
     assert (d1 - ref_dp).abs().max().item() <= 1e-4 * ref_dp.abs().max().item() + 1e-7
     model._check_range("stream-K test")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["pythia-2.8b", "pythia-12b"])
+def test_row_attention_matches_tile_kernel(name, monkeypatch):
+    """attention_row_kernel (one query row per sequence: last-position sites,
+    every sweep's trimmed last layer) against attention_mfma_kernel
+    (TVR_ROW_ATTN=0) at d_head 80 / 128, and against the CPU oracle: a layer
+    sweep's Δprob / accuracy, a clean forward's last-row logits and a CIE
+    (whose last layer is single-row)."""
+    cfg = tvr_amd.get_config(name).with_(n_layers=3)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok)
+    oracle = make_oracle(cfg, sd, tok)
+    task = list(tvr_amd.tasks.letter_to_caps)[:20]
+    arrow = tvr_amd.tasks.ARROW
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 2, 4, seed=1234)
+    answers = [int(t) for t in model.forward_clean(prompts, topk=1)["topk"][:, 0].tolist()]
+    g = torch.Generator().manual_seed(5)
+    mean = (torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5).cuda()
+    layered = tvr_amd.gather_head_activations_to_layers(mean)
+    out = {}
+    for ra in ("1", "0"):
+        monkeypatch.setenv("TVR_ROW_ATTN", ra)
+        logits = model.forward_clean(prompts, topk=1, return_logits=True)["logits"].cpu().double()
+        dp = tvr_amd.apply_layered_vectors_to_zero_shot_by_probability(layered, task, arrow, model=model)
+        acc = tvr_amd.apply_layered_vectors_to_zero_shot(layered, task, arrow, model=model)
+        cie = tvr_amd.experiments.causal_indirect_effect_sums(mean, prompts, answers, model).cpu().double()
+        out[ra] = (logits, dp.cpu().double(), acc, cie)
+    (l1, d1, a1, c1), (l0, d0, a0, c0) = out["1"], out["0"]
+    assert ((l1 - l0).abs().max() / l0.abs().max()).item() < 1e-5
+    assert (d1 - d0).abs().max().item() <= 1e-4 * d0.abs().max().item() + 1e-7
+    assert a1 == a0
+    assert (c1 - c0).abs().max().item() <= 1e-4 * c0.abs().max().item() + 1e-7
+    ref = torch.stack([oracle.forward(torch.tensor([p]))[0, -1] for p in prompts]).double()
+    assert ((l1 - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    ref_dp = R.apply_layered_vectors_to_zero_shot_by_probability(layered.cpu(), task, arrow, oracle).double()
+    assert (d1 - ref_dp).abs().max().item() <= 1e-4 * ref_dp.abs().max().item() + 1e-7
+    assert a1 == R.apply_layered_vectors_to_zero_shot(layered.cpu(), task, arrow, oracle)
+    model._check_range("row attention test")
