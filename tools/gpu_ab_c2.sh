@@ -1,10 +1,13 @@
-# C2 layer-sweep anatomy with stream-K on and off (same box, interleaved):
+# C2 layer-sweep anatomy under the small-M switches (same box, interleaved):
+# TVR_STREAM_K (stream-K GEMM launches) x TVR_ROW_ATTN (single-query attention).
 #   gpurun -- 'bash tools/gpu_ab_c2.sh <tag>'
 TAG=${1:?tag}
 mkdir -p gpurun_out
 for i in 1 2; do
-  for sk in 1 0; do
-    TVR_STREAM_K=$sk timeout -k 10 200 python -u tools/c2_probe.py --reps 3 > gpurun_out/c2_${TAG}_sk${sk}_$i.json 2> gpurun_out/c2_${TAG}_sk${sk}_$i.err || exit $?
-    echo "sk=$sk: $(cut -c1-200 gpurun_out/c2_${TAG}_sk${sk}_$i.json)"
+  for v in "1 1" "0 0" "1 0" "0 1"; do
+    set -- $v
+    TVR_STREAM_K=$1 TVR_ROW_ATTN=$2 timeout -k 10 200 python -u tools/c2_probe.py --reps 3 \
+      > gpurun_out/c2_${TAG}_sk$1_ra$2_$i.json 2> gpurun_out/c2_${TAG}_sk$1_ra$2_$i.err || exit $?
+    echo "sk=$1 ra=$2: $(cut -c1-120 gpurun_out/c2_${TAG}_sk$1_ra$2_$i.json)"
   done
 done
