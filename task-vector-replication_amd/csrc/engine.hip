@@ -888,9 +888,12 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
 // the n_last rows listed in d_last only (~5% of a CIE sweep's FLOPs saved).
 // d_seqs must carry q0 = n - 1.  write_out = false skips the second projection
 // (nothing downstream reads the final residual).
+// row_from: the sequences [row_from, n_seqs) query their last row only (the
+// single-query kernel); the ones before it (a fused sweep's clean sequences,
+// whose every row the trace keeps: q0 = 0) go to the MFMA kernel.
 int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int maxT, Acts& a,
                         const float* cache_qkv, const int32_t* d_last, int n_last, bool write_out,
-                        float* zf, hipStream_t st, bool zf_last = false, int zf_rows = INT_MAX) {
+                        float* zf, hipStream_t st, bool zf_last = false, int zf_rows = INT_MAX, int row_from = 0) {
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
@@ -906,8 +909,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e1.out_rows = d_last;
   TVR_TRY(launch_w1(m, l, a.xn, n_last, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
-  // every sequence queries its last row only (d_seqs carries q0 = n - 1): the single-query kernel
-  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows, 0));
+  TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows,
+                           row_from));
   ps.done(TVR_HBM_ATTENTION, attention_bytes(d, n_last, R, a.fmt, zf ? std::min(n_last, zf_rows) : 0));
   if (!write_out) return TVR_OK;
   GemmEpi e2{};
@@ -1158,13 +1161,13 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     mats.push_back(&m->w2[l]); sizes.push_back(n2);
   }
   mats.push_back(&m->wu); sizes.push_back(nu);
-  std::vector<float> scale(mats.size(), 1.0f);
   if (mode == TVR_GEMM_BF16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
     for (int l = 0; l < L; ++l) {
       mats.push_back(nullptr);
       sizes.push_back(nqk);
     }
   }
+  std::vector<float> scale(mats.size(), 1.0f);  // sized after the Q / K entries: one per matrix
   if (mode == TVR_GEMM_X2F16 || mode == TVR_GEMM_BF16) {
     // one power-of-two scale per matrix from its largest magnitude
     unsigned* d_max = nullptr;
@@ -2026,7 +2029,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
       TVR_TRY(run_block_lin(l, Rl, cache, zf));
     } else if (l == L - 1) {
       TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), nc + cnt_le[l], maxT, a, cache,
-                                  (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc));
+                                  (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc,
+                                  nc));
     } else {
       TVR_TRY(run_block(m, l, Rl, d_seqs, nc + cnt_le[l], maxT, a, a.qkv, cache, zf, st, false, Rc,
                         single_rows ? nc : INT_MAX));
