@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 9
+#define TVR_ABI_VERSION 10
 
 enum tvr_status {
   TVR_OK = 0,
@@ -310,6 +310,15 @@ typedef struct tvr_hbm_stats {
   double bytes[6];  /* algorithmic bytes summed */
 } tvr_hbm_stats;
 int tvr_profile_read_hbm(tvr_model* model, tvr_hbm_stats* out);
+
+/* The launch plan the engine uses for one planar GEMM of M x N x K
+ * (gemm_pingpong_kernel, 256 x 256 tiles; engine.hip plan_pp): out[0] k-split
+ * of the whole launch, out[1] first tile of a split tail (0: none), out[2] the
+ * tail's split, out[3] first stream-K tile (-1: none), out[4] stream-K blocks.
+ * gemm_mode: TVR_GEMM_X2F16 or TVR_GEMM_BF16; gelu != 0: the QKV + MLP-in
+ * launch (GELU epilogue).  Host-only, no device call (diagnostics, CPU tests).
+ * (ABI 10) */
+int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t gelu, int32_t* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);
  * the weight planes of the split / bf16 modes are not included (X3BF16 6 B,

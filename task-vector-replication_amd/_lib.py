@@ -70,7 +70,7 @@ class CHbmStats(ctypes.Structure):
 HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats", "lin_entry")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 9  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 10  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
@@ -128,6 +128,8 @@ SIGNATURES = {
     "tvr_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "tvr_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CKernelStats)]),
     "tvr_profile_read_hbm": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CHbmStats)]),
+    "tvr_gemm_plan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_void_p]),
 }
 
 OPS_PATH = LIB_PATH.parent / OPS_NAME

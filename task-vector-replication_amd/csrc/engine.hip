@@ -16,9 +16,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "tvr.h"
@@ -96,6 +98,14 @@ struct MatW {
   }
 };
 
+// Launch plan of a planar GEMM (plan_pp).
+struct PpPlan {
+  int ksplit = 1;    // whole launch
+  int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
+  int tail_split = 1;
+  int sk_base = -1;  // >= 0: tiles [0, sk_base) plain, the rest stream-K over sk_blocks blocks
+  int sk_blocks = 0;
+};
 }  // namespace
 
 struct tvr_model {
@@ -138,6 +148,7 @@ struct tvr_model {
   uint16_t* lin_planes = nullptr;  // layer l at (l - 1) * NPL * H * D1 * KP halves
   float* lin_c1 = nullptr;         // [L][D1]
   std::vector<float> lin_scale;    // per layer: X2F16 plane scale (1 for BF16)
+  std::unordered_map<uint64_t, PpPlan> plans;  // plan_pp_cached: GEMM launch plans per shape
 };
 
 struct tvr_trace {
@@ -425,26 +436,75 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
 }
 
 // Launch shape of a planar GEMM on 256 CUs (gemm_pingpong_kernel, one block
-// per CU).  Fewer than 256 tiles: stream-K over the whole launch (every CU
-// gets the same share of the k-iterations) when the round it saves beats two
-// partial tile epilogues per block and the fix-up's HBM round trip (else
-// split-K when fewer than 192); otherwise, when the last round would run
-// partly empty, its tiles (the raster's last ones) go stream-K (or split-K)
-// over all CUs when that pays.  Costs in us (tools/gemm_split_probe
-// anatomy: ~2.2 us per x2f16 k-tile per block, ~15 us per partial segment's
-// prologue + epilogue, fix-up at ~4 TB/s over the partials).
-struct PpPlan {
-  int ksplit = 1;    // whole launch
-  int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
-  int tail_split = 1;
-  int sk_base = -1;  // >= 0: tiles [0, sk_base) plain, the rest stream-K over sk_blocks blocks
-  int sk_blocks = 0;
+// per CU): the whole launch plain, the whole launch split over K (fp32
+// partials + splitk_reduce_kernel), or its last tiles split (a partly empty
+// last round), and — opt-in, TVR_STREAM_K=1 — stream-K for the last round.
+// Launches of up to 1,024 tiles (the small-M layer sweeps: C2's M = 156 + 52 l
+// rows) are planned by simulating the dispatch (plan_sim): blocks in
+// blockIdx order through the kernel's XCD remap onto the first free of 256
+// CUs, a block costing its k-tiles at a rate set by its tile's real rows (a
+// wave group skips the MFMAs of its padding 16-row slices; the staging
+// remains) plus prologue and epilogue, a split plan the reduce's partial round
+// trip on top.  Larger launches keep the round heuristic (their full rounds
+// dominate).  Costs in us: profiles/c2trace_r03f (per-dispatch trace of a C2
+// sweep: 1.5-2.2 us per x2f16 k-tile per block, reduce at ~5 TB/s).
+// stream-K is opt-in: on the C2 sweeps it measured slower than the split-K
+// plan (O + MLP-out 8.2 vs 5.7 ms per sweep) and equal on C3
+// (profiles/r03/c2_stream_k_ab.txt)
+bool sk_enabled() {
+  const char* e = getenv("TVR_STREAM_K");
+  return e && std::string(e) == "1";
+}
+
+struct PlanCost {
+  double kt_us, pro_us, epi_us, part_us;
 };
-bool sk_enabled() { return env_flag("TVR_STREAM_K"); }
-PpPlan plan_pp(int M, int N, int K, int a_fmt) {
+
+// Simulated time (us) of tiles [t0, t0 + cnt) of the raster launched with S
+// blocks per tile (S = 1: plain epilogue; S > 1: partial tiles, no reduce).
+double plan_sim(int M, int N, int nkt, int t0, int cnt, int S, const PlanCost& pc) {
+  const int nbm = (M + 255) / 256, nbn = (N + 255) / 256, gm = pp_group_m(N);
+  const int nb = cnt * S, P = 256;
+  std::vector<double> cu(P, 0.0);  // CU free times (a min-heap)
+  auto remap = [](int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  };
+  double end = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    const int wgs = remap(b, nb), lt = wgs / S, split = wgs - lt * S;
+    int m0, n0;
+    pp_tile_coords(t0 + lt, nbm, nbn, m0, n0, gm);
+    (void)n0;
+    const int rows = std::min(256, M - m0);
+    const int s0 = (std::min(rows, 128) + 15) / 16, s1 = (std::max(rows - 128, 0) + 15) / 16;
+    const double frac = 0.3 + 0.7 * std::max(s0, s1) / 8.0;
+    const int kb = (int)((long long)split * nkt / S), ke = (int)((long long)(split + 1) * nkt / S);
+    const double dur = pc.pro_us + (ke - kb) * pc.kt_us * frac + (S > 1 ? pc.part_us : pc.epi_us);
+    std::pop_heap(cu.begin(), cu.end(), std::greater<double>());
+    cu.back() += dur;
+    end = std::max(end, cu.back());
+    std::push_heap(cu.begin(), cu.end(), std::greater<double>());
+  }
+  return end;
+}
+
+// the split-K reduce of tiles [t0, t0 + cnt) over S partials: launch + partials read + output written
+double plan_reduce_us(int M, int N, int t0, int cnt, int S) {
+  const int nbm = (M + 255) / 256, nbn = (N + 255) / 256, gm = pp_group_m(N);
+  double rows = 0.0;
+  for (int t = t0; t < t0 + cnt; ++t) {
+    int m0, n0;
+    pp_tile_coords(t, nbm, nbn, m0, n0, gm);
+    rows += std::min(256, M - m0) * (double)std::min(256, N - n0);
+  }
+  return 4.0 + rows * 4.0 * (2.0 * S + 1.0) / 5.0e6;  // partials written (by the GEMM) + read, output written
+}
+
+PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi) {
   PpPlan p;
   const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_X2F16 ? 32 : 64);
-  const double kt_us = a_fmt == ACT_X2F16 ? 2.2 : 1.5, seg_us = 15.0, epi_us = 10.0;
+  const double kt_us = a_fmt == ACT_X2F16 ? 1.9 : 1.3, seg_us = 15.0, epi_us = 10.0;
   // stream-K of `cnt` tiles over min(256, iterations) blocks vs one plain round
   auto sk_us = [&](int cnt) {
     const int G = (int)std::min<long long>(256, (long long)cnt * nkt);
@@ -460,13 +520,34 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt) {
       return p;
     }
   }
-  if (tiles < 192) {
-    p.ksplit = std::max(1, std::min(std::min(256 / tiles, nkt / 8), 16));
+  if (tiles <= 1024) {
+    const PlanCost pc{kt_us, 3.0, epi == EPI_SPLIT_GELU_ACT ? 15.0 : 10.0, 7.0};
+    double best = plan_sim(M, N, nkt, 0, tiles, 1, pc);
+    for (int S = 2; S <= 16 && nkt / S >= 8 && tiles * S <= 8192; ++S) {
+      const double c = plan_sim(M, N, nkt, 0, tiles, S, pc) + plan_reduce_us(M, N, 0, tiles, S);
+      if (c < best * 0.97) {  // a split must win clearly: the model is approximate
+        best = c;
+        p.ksplit = S;
+      }
+    }
+    if (tiles > 256) {
+      const int base = 256 * ((tiles - 1) / 256), cnt = tiles - base;
+      const double head = plan_sim(M, N, nkt, 0, base, 1, pc);
+      for (int S = 2; S <= 16 && nkt / S >= 8; ++S) {
+        const double c = head + plan_sim(M, N, nkt, base, cnt, S, pc) + plan_reduce_us(M, N, base, cnt, S);
+        if (c < best * 0.97) {
+          best = c;
+          p.ksplit = 1;
+          p.tail_base = base;
+          p.tail_split = S;
+        }
+      }
+    }
     return p;
   }
   const int rounds = (tiles + 255) / 256;
   const int tb = tiles - 256 * (rounds - 1);
-  if (rounds < 2 || tb > 224) return p;
+  if (tb > 224) return p;
   int best = 1;
   double br = 1.0;
   for (int s = 2; s <= 16 && nkt / s >= 8; ++s) {
@@ -484,6 +565,20 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt) {
     p.tail_base = 256 * (rounds - 1);
     p.tail_split = best;
   }
+  return p;
+}
+
+// plan_pp, cached per launch shape on the model (the sweeps repeat their
+// per-layer shapes: the simulation runs once per shape)
+PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi) {
+  const uint64_t key = ((uint64_t)(uint32_t)M << 32) ^ ((uint64_t)(uint32_t)N << 12) ^ ((uint64_t)(uint32_t)K << 3) ^
+                       ((uint64_t)(a_fmt & 3) << 1) ^ (uint64_t)(epi == EPI_SPLIT_GELU_ACT) ^
+                       ((uint64_t)sk_enabled() << 63);
+  auto it = m->plans.find(key);
+  if (it != m->plans.end()) return it->second;
+  const PpPlan p = plan_pp(M, N, K, a_fmt, epi);
+  if (m->plans.size() > 4096) m->plans.clear();
+  m->plans.emplace(key, p);
   return p;
 }
 
@@ -543,7 +638,7 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
 #undef TVR_SK
     } else {
       PpPlan plan;
-      if (m && vec && epi != EPI_STATS) plan = plan_pp(M, N, K, a_fmt);
+      if (m && vec && epi != EPI_STATS) plan = plan_pp_cached(m, M, N, K, a_fmt, epi);
       if (plan.sk_base >= 0) {
         if (plan.sk_base > 0) launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.sk_base, true, st);
         TVR_TRY(launch_pp_sk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.sk_base,
@@ -2027,7 +2122,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     float* zf = fused ? trace->z + l * tstride : nullptr;  // the clean rows' hook_z (rows < Rc)
     if (use_lin[l]) {
       TVR_TRY(run_block_lin(l, Rl, cache, zf));
-    } else if (l == L - 1) {
+    } else if (l == L - 1 && Rc + cnt_le[l] < Rl) {  // (every row a last row, e.g. C2's: the plain block)
       TVR_TRY(run_block_last_rows(m, l, Rl, (const SeqDesc*)(base + o_seqs_last), nc + cnt_le[l], maxT, a, cache,
                                   (const int32_t*)(base + o_last_sorted), Rc + cnt_le[l], true, zf, st, false, Rc,
                                   nc));
@@ -2050,6 +2145,20 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     TVR_TRY(run_final(m, a.resid, (const int32_t*)(base + o_clast), (const int32_t*)(base + o_ctg), nc,
                       (float*)(base + o_xf), (float*)(base + o_lg), trace->p_prob, trace->p_topk, trace->p_k,
                       nullptr, fmt, st));
+  return TVR_OK;
+}
+
+int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t gelu, int32_t* out) {
+  if (M <= 0 || N <= 0 || K <= 0 || !out || (gemm_mode != TVR_GEMM_X2F16 && gemm_mode != TVR_GEMM_BF16))
+    return fail(TVR_ERR_INVALID, "tvr_gemm_plan: bad argument");
+  const int fmt = gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : ACT_BF16;
+  if (K % (fmt == ACT_X2F16 ? 32 : 64) != 0) return fail(TVR_ERR_UNSUPPORTED, "tvr_gemm_plan: K not a k-tile multiple");
+  const PpPlan p = plan_pp(M, N, K, fmt, gelu ? EPI_SPLIT_GELU_ACT : EPI_RESID);
+  out[0] = p.ksplit;
+  out[1] = p.tail_base;
+  out[2] = p.tail_split;
+  out[3] = p.sk_base;
+  out[4] = p.sk_blocks;
   return TVR_OK;
 }
 

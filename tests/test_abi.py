@@ -34,7 +34,7 @@ def test_binding_covers_header():
 
 def test_version_and_errors_without_gpu():
     lib = tvr_amd._lib.load()
-    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 9
+    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 10
     assert b"gfx950" in lib.tvr_version()
     # argument validation runs before any device call
     out = ctypes.c_void_p()
