@@ -9,6 +9,6 @@ i=0
 for v in "$@"; do
   i=$((i + 1))
   echo "== $i $v" | tee -a $OUT/summary.txt
-  env $v timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-f32-leg > $OUT/run$i.json 2> $OUT/run$i.err || exit $?
+  env $v timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-f32-leg --configs= > $OUT/run$i.json 2> $OUT/run$i.err || exit $?
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; h=d.get('hbm_kernels') or {}; print(d['value'], d['ms_per_step'], r['achieved'], {k: v['achieved_tflops'] for k, v in r['variants'].items()}, {k: (v['avg_launch_us'], v['achieved_gbps']) for k, v in h.items() if isinstance(v, dict)})" $OUT/run$i.json | tee -a $OUT/summary.txt
 done
