@@ -27,6 +27,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "gemm_planar.hpp"
 #include "kernels.hpp"
 
 namespace tvr {
@@ -45,8 +46,16 @@ constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 // zf (the extraction's capture reads nothing else), instead of every row;
 // otherwise rows below zf_rows only (a fused clean + patch sweep traces its
 // clean rows, which come first).
-template <int FMT, int DH, int NKT>
-__global__ void __launch_bounds__(64 * ATTM_WAVES, (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
+// STAGE (NKT == 1 only: T <= 16, the C3 / C1 sweeps): the wave's Q, K and V
+// head slices are first copied into LDS by LDS-DMA (global_load_lds_dwordx4),
+// lane l moving 16-B chunk l of a packed [16 rows][DH] image, so each
+// instruction reads whole 16-B chunks of consecutive rows' slices (DH * 4 B
+// contiguous per row) instead of 16 rows x 4 lane-group chunks, and V's
+// fragments come from LDS instead of 4-B global loads; the fragments are then
+// read from LDS in the MFMA layout.  No block barrier: each wave owns its
+// region and waits for its own DMAs (vmcnt).
+template <int FMT, int DH, int NKT, bool STAGE = false>
+__global__ void __launch_bounds__(64 * ATTM_WAVES, STAGE ? 2 : (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
 attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
                       const SeqDesc* __restrict__ seqs, int n_seqs, int n_heads, void* __restrict__ z, int ldz,
                       float* __restrict__ zf, int ldzf, int zf_last, int zf_rows, unsigned* __restrict__ flag,
@@ -58,6 +67,9 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   constexpr bool LONG = NKT == 0;
   constexpr int MAXKT = LONG ? 8 : NKT;
   static_assert(DH % 16 == 0 && DH <= 128 && MAXKT * 16 <= ATT_MAX_T, "d_head / key tiles");
+  static_assert(!STAGE || NKT == 1, "LDS staging: one key tile");
+  constexpr int SMAT = 16 * DH;  // floats of one staged [16][DH] matrix
+  __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * 3 * SMAT : 4];
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
   if (pair >= n_seqs * n_heads) return;  // a whole wave; nothing below synchronises
@@ -75,7 +87,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   auto row_of = [&](int j) -> const float* {
     return j < sd.p0 ? pfx + (size_t)(sd.cache_row + j) * ldp : qkv + (size_t)(sd.row0 + j - sd.p0) * ldq;
   };
-  // dims [g CH, g CH + CH) of a Q or K head row, rotated for position pos
+  // dims [g CH, g CH + CH) of a Q or K head row (global or staged), rotated for position pos
   auto load_chunk = [&](const float* r, int pos, float (&x)[CH]) {
 #pragma unroll
     for (int c = 0; c < CH; c += 4) {
@@ -95,11 +107,30 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     }
   };
 
+  float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * 3 * SMAT : 0);
+  if constexpr (STAGE) {
+    // rows: Q = the query tile's rows (padding repeats the last), K / V = keys 0 .. 15 (clamped to T - 1);
+    // instruction i of matrix m moves chunks 64 i + lane = (row, c) of the packed image
+#pragma unroll
+    for (int mat = 0; mat < 3; ++mat) {
+#pragma unroll
+      for (int i = 0; i < DH / 16; ++i) {
+        const int id = i * 64 + lane, row = id / CH, c = id - row * CH;
+        const float* src = mat == 0 ? qkv + (size_t)(sd.row0 + min(sd.q0 + row, sd.n - 1)) * ldq
+                                    : row_of(min(row, T - 1)) + mat * d;
+        glds16(src + h * DH + 4 * c, stg + mat * SMAT + i * 256);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   for (int q0 = sd.q0; q0 < sd.n; q0 += 16) {
     // this lane's query column: relative row q0 + li (padding reuses the last row)
     const int qi = min(q0 + li, sd.n - 1);
     float qf[CH];
-    load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
+    if constexpr (STAGE)
+      load_chunk(stg + li * DH, sd.p0 + qi, qf);  // T <= 16: one query tile, staged from q0
+    else
+      load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
     f4 zt[NDT];
     if constexpr (LONG) {
       const int qpos = sd.p0 + q0 + li;  // this lane's query (absolute position)
@@ -186,7 +217,8 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
       if constexpr (NKT == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float* vr = row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
+          const float* vr = STAGE ? stg + 2 * SMAT + (4 * g + r) * DH + li
+                                  : row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
         }
@@ -199,7 +231,10 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         if (kt < nkt) {
           const int kj = min(16 * kt + li, T - 1);
           float kf[CH];
-          load_chunk(row_of(kj) + d + h * DH, kj, kf);
+          if constexpr (STAGE)
+            load_chunk(stg + SMAT + li * DH, kj, kf);  // staged row li = key min(li, T - 1)
+          else
+            load_chunk(row_of(kj) + d + h * DH, kj, kf);
           // two accumulation chains (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
           f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

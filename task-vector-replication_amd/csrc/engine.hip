@@ -869,12 +869,15 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
   // key tiles in registers: 1 / 2 / 4 / 8, or 0 = longer than 128 (chunked online softmax)
   const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 0;
-#define TVR_ATTM(F, DHV, NK)                                                                                        \
-  hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
+  // one key tile: Q / K / V slices staged through LDS by LDS-DMA (TVR_ATT_STAGE=0: direct loads, A/B)
+  const bool stage = env_flag("TVR_ATT_STAGE");
+#define TVR_ATTM(F, DHV, NK, ...)                                                                                   \
+  hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK __VA_OPT__(,) __VA_ARGS__>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
                      inv_scale)
 #define TVR_ATTM_NK(F, DHV)                                                                     \
-  if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                            \
+  if (nkt == 1 && stage) TVR_ATTM(F, DHV, 1, (DHV <= 80));  /* d_head 128: 98 KB per block, not staged */ \
+  else if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                       \
   else if (nkt == 2) TVR_ATTM(F, DHV, 2);                                                       \
   else if (nkt == 4) TVR_ATTM(F, DHV, 4);                                                       \
   else if (nkt == 8) TVR_ATTM(F, DHV, 8);                                                       \
