@@ -446,8 +446,8 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
 // wave group skips the MFMAs of its padding 16-row slices; the staging
 // remains) plus prologue and epilogue, a split plan the reduce's partial round
 // trip on top.  Larger launches keep the round heuristic (their full rounds
-// dominate).  Costs in us: profiles/c2trace_r03f (per-dispatch trace of a C2
-// sweep: 1.5-2.2 us per x2f16 k-tile per block, reduce at ~5 TB/s).
+// dominate).  Costs in us: profiles/r03/c2_sweep_dispatches_r03f.txt (a C2
+// sweep per dispatch: 1.5-2.2 us per x2f16 k-tile per block, reduce at ~5 TB/s).
 // stream-K is opt-in: on the C2 sweeps it measured slower than the split-K
 // plan (O + MLP-out 8.2 vs 5.7 ms per sweep) and equal on C3
 // (profiles/r03/c2_stream_k_ab.txt)
