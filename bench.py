@@ -106,10 +106,10 @@ def parse():
     ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks on one GPU")
-    ap.add_argument("--configs", default="C2,C5",
+    ap.add_argument("--configs", default="C2,C4,C5",
                     help="N=1: the other BASELINE.json configs timed after the headline, reported under 'configs' "
-                         "(C2 = the Pythia-2.8B layer sweeps on the headline model, C5 = the Pythia-12B 36x40 "
-                         "10-shot CIE sweep); '' skips them")
+                         "(C2 = the Pythia-2.8B layer sweeps on the headline model, C4 = the Pythia-6.9B bf16 "
+                         "function-vector suite per task, C5 = the Pythia-12B 36x40 10-shot CIE sweep); '' skips them")
     ap.add_argument("--launch-check", dest="launch_check", action="store_true",
                     help="only the rank launch, rendezvous and max-over-ranks timing (no GPU work; CPU test)")
     return ap.parse_args()
@@ -292,6 +292,53 @@ def config_c5(args, dev, peak):
             "value": round(rate, 2), "unit": "patched prompts/s", "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak, 4),
             "model_build_s": round(build_s, 1)}
+
+
+def config_c4(args, dev, n_tasks=3):
+    """C4: Pythia-6.9B in the north star's bf16 configuration,
+    the function-vector suite per synthetic 50-pair task — extraction over 512
+    five-shot prompts (a1), the 32 x 32 CIE over 12 shuffled prompts (a7), the
+    function vector of the top-10 heads (a10) added at every layer over the 50
+    zero-shot prompts, top-5 accuracy (a11) — through the sharded entry points
+    (one process: the plain functions).  One warm task, then ``n_tasks`` timed
+    (tools/bench_configs.py --configs C4 runs the 20-task suite)."""
+    import random
+    import tvr_amd
+    from tvr_amd import distributed as D
+    from tvr_amd import experiments as E
+    t0 = time.time()
+    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device=dev, seed=0, gemm="bf16")
+    build_s = time.time() - t0
+    arrow = tvr_amd.tasks.ARROW
+
+    def one(ti):
+        task = tvr_amd.tasks.synthetic_task(50, model.cfg.d_vocab, seed=100 + ti)
+        random.seed(ti)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, task, arrow, ",", 512, 5)
+        mean = D.mean_activation_sharded(ex_prompts, model)
+        prompts, answers = E.generate_shuffled_prompts(task, model, 12, 5, arrow)
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        cie = D.cie_heads_sharded(mean, prompts, answers, model)
+        torch.cuda.synchronize()
+        tc = time.perf_counter() - tc
+        fv = E.assemble_task_vector(mean, cie, 10, 10)
+        acc = D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, task, 5, model)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t, tc, acc
+
+    one(0)  # warm: trace / workspace sizing
+    runs = [one(ti) for ti in range(1, n_tasks + 1)]
+    L, H = model.cfg.n_layers, model.cfg.n_heads
+    del model
+    torch.cuda.empty_cache()
+    return {"workload": f"pythia-6.9b bf16 FV suite per 50-pair task: extraction 512 x 5-shot, CIE {L}x{H} over 12 "
+                        "prompts, top-10-head FV added at every layer over 50 zero-shot prompts (top-5)",
+            "gemm": "bf16", "tasks_timed": n_tasks, "s_per_task": round(sum(r[0] for r in runs) / n_tasks, 3),
+            "cie_patched_prompts_per_s": round(sum(12 * L * H / r[1] for r in runs) / n_tasks, 1),
+            "fv_top5_acc_by_layer_last_task": runs[-1][2], "model_build_s": round(build_s, 1)}
 
 
 def cpu_baseline(args, cfg, prompts, answers, mean, model):
@@ -588,10 +635,17 @@ def main():
                 log(f"C2: {out['configs']['C2']['accuracy']['sites_per_s']} / {out['configs']['C2']['dprob']['sites_per_s']} sites/s")
             except Exception as e:  # a config leg never voids the headline line
                 out["configs"]["C2"] = {"error": f"{type(e).__name__}: {e}"}
-        if "C5" in which:
+        if which & {"C4", "C5"}:
             del model
             torch.cuda.empty_cache()
             model = None
+        if "C4" in which:
+            try:
+                out["configs"]["C4"] = config_c4(args, dev)
+                log(f"C4: {out['configs']['C4']['s_per_task']} s/task")
+            except Exception as e:
+                out["configs"]["C4"] = {"error": f"{type(e).__name__}: {e}"}
+        if "C5" in which:
             try:
                 out["configs"]["C5"] = config_c5(args, dev, peak)
                 log(f"C5: {out['configs']['C5']['value']} patched prompts/s")

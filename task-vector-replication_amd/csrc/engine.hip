@@ -793,8 +793,11 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
 }
 
 // y: fp32 [rows][ldy] (ACT_F32) or a planar activation format
+// copy: rows < copy_rows of x also go there unchanged (same stride; a fused
+// sweep's clean rows into the trace's hook_resid_pre)
 int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
-                 int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr, float2* stats = nullptr) {
+                 int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr, float2* stats = nullptr,
+                 float* copy = nullptr, int copy_rows = 0) {
   if (rows <= 0) return TVR_OK;
   ProfSpan ps(m, st);
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
@@ -802,14 +805,17 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
   if (fmt == ACT_X2F16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
+                       copy_rows);
   else if (fmt == ACT_BF16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
+                       copy_rows);
   else
-    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats);
+    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
+                       copy_rows);
   TVR_HIP(hipGetLastError());
   // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element)
-  ps.done(TVR_HBM_LNPRE, (double)rows * d * 8.0);
+  ps.done(TVR_HBM_LNPRE, (double)rows * d * 8.0 + (copy ? (double)std::min(rows, copy_rows) * d * 4.0 : 0.0));
   return TVR_OK;
 }
 
@@ -821,6 +827,12 @@ struct Acts {
   float* qkv;     // [R][3d]
   float* a2;      // [R][K2]  (z | gelu(mlp-in))
   int fmt;
+  // a fused clean + patch sweep: rows < mirror_rows (the clean rows) of the
+  // layer's resid_pre (LayerNorm's input) and qkv (the QKV epilogue's fp32
+  // columns) are also written to the trace by the kernels producing them
+  float* resid_mirror = nullptr;
+  float* qkv_mirror = nullptr;
+  int mirror_rows = 0;
 };
 
 // z: the z columns of a2 (fp32 or activation format fmt); zf: optional fp32 copy [rows][d].
@@ -912,6 +924,8 @@ GemmEpi epi_qkv_mlpin(tvr_model* m, const float* b1, float* qkv, const Acts& a) 
   e.out0 = qkv;
   e.ld0 = 3 * d;
   e.n_split = 3 * d;
+  e.out0m = a.qkv_mirror;
+  e.mirror_rows = a.mirror_rows;
   if (planar) {
     e.out1h = reinterpret_cast<uint16_t*>(a.a2) + d;
     e.ld1h = 2 * m->K2;
@@ -950,6 +964,8 @@ int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const G
     e.ld0 = ep.ld0;
     e.a_rows = ep.a_rows;
     e.out_rows = ep.out_rows;
+    e.out0m = ep.out0m;
+    e.mirror_rows = ep.mirror_rows;
     TVR_TRY(launch_gemm(EPI_BIAS, static_cast<const uint16_t*>(xn) + d, d, ACT_F16,
                         m->w1qk[l].rows((size_t)c0 * d), d, M, nqk, d, e, st, m));
     if (nqk == N) return TVR_OK;
@@ -958,6 +974,7 @@ int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const G
   if (nqk > 0) {
     e.bias = ep.bias ? ep.bias + nqk : nullptr;
     e.out0 = ep.out0 + nqk;
+    if (ep.out0m) e.out0m = ep.out0m + nqk;
     e.n_split = ep.n_split - nqk;
   }
   return launch_gemm(epi, xn, d, fmt, m->w1[l].rows((size_t)(c0 + nqk) * d), d, M, N - nqk, d, e, st, m);
@@ -970,7 +987,8 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m, nullptr, a.resid_mirror,
+                       a.mirror_rows));
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
   TVR_TRY(launch_w1(m, l, a.xn, R, 0, m->D1, e1, st));
   ProfSpan ps(m, st);
@@ -995,7 +1013,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   const tvr_config& c = m->cfg;
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
-  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m));
+  TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m, nullptr, a.resid_mirror,
+                       a.mirror_rows));
   GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row (all below n_split: no GELU)
   kv.bias = w.b1 + d;
   kv.out0 = a.qkv + d;
@@ -2013,7 +2032,9 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   auto enter = [&](int l) -> int {
     const int k0 = l > 0 ? cnt_le[l - 1] : 0, k1 = cnt_le[l];
     if (k1 <= k0) return TVR_OK;
-    const float* snap = trace->resid + (size_t)l * tstride;
+    // the clean rows' hook_resid_pre: the live rows [0, Rc) in a fused sweep (the trace's copy is written by
+    // this layer's LayerNorm, after the entry), else the trace
+    const float* snap = fused ? a.resid : trace->resid + (size_t)l * tstride;
     const float* zsnap = l > 0 ? trace->z + (size_t)(l - 1) * tstride : nullptr;
     const float* w2 = l > 0 ? m->layers[l - 1].w2 : nullptr;
     const dim3 eg(k1 - k0, (d + ENTRY_THREADS - 1) / ENTRY_THREADS);
@@ -2066,7 +2087,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   auto run_block_lin = [&](int l, int Rl, const float* cache, float* zf) -> int {
     const tvr_layer_weights& w = m->layers[l];
     const int Rp = Rc + rows_le[l - 1], D1 = m->D1;
-    TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, Rl, d, c.ln_eps, fmt, st, m, lnstats));
+    TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, Rl, d, c.ln_eps, fmt, st, m, lnstats, a.resid_mirror,
+                         a.mirror_rows));
     GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);
     e1.raw = raw_h;
     e1.raw_rows = Rc;
@@ -2115,12 +2137,15 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   };
 
   for (int l = 0; l < L; ++l) {
-    if (fused)  // hook_resid_pre of the clean rows (the entries below read it from the trace)
-      TVR_HIP(hipMemcpyAsync(trace->resid + l * tstride, a.resid, rbytes, hipMemcpyDeviceToDevice, st));
-    TVR_TRY(enter(l));
     const int Rl = Rc + rows_le[l];
-    if (Rl == 0) continue;
     float* tqkv = trace->qkv + (size_t)l * 3 * tstride;
+    if (fused) {  // the clean rows' hook_resid_pre / K,V cache go to the trace from the kernels writing them
+      a.resid_mirror = trace->resid + l * tstride;
+      a.qkv_mirror = tqkv;
+      a.mirror_rows = Rc;
+    }
+    TVR_TRY(enter(l));
+    if (Rl == 0) continue;
     const float* cache = fused ? a.qkv : tqkv;
     float* zf = fused ? trace->z + l * tstride : nullptr;  // the clean rows' hook_z (rows < Rc)
     if (use_lin[l]) {
@@ -2134,9 +2159,9 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
                         single_rows ? nc : INT_MAX));
       TVR_TRY(run_block_out(m, l, Rl, a, st));
     }
-    if (fused)
-      TVR_HIP(hipMemcpyAsync(tqkv, a.qkv, 3 * rbytes, hipMemcpyDeviceToDevice, st));
   }
+  a.resid_mirror = a.qkv_mirror = nullptr;
+  a.mirror_rows = 0;
   if (fused) {
     TVR_HIP(hipMemcpyAsync(trace->resid + L * tstride, a.resid, rbytes, hipMemcpyDeviceToDevice, st));
     trace->pending = false;

@@ -107,6 +107,11 @@ struct GemmEpi {
   float* raw;
   int raw_rows;
   int ld_raw;
+  // fp32 (out0) columns of output rows < mirror_rows also go to out0m (same
+  // row stride ld0): a fused clean + patch sweep's clean rows into the trace's
+  // K / V cache (EPI_BIAS, EPI_SPLIT_GELU, EPI_SPLIT_GELU_ACT below n_split)
+  float* out0m;
+  int mirror_rows;
   // EPI_BIAS planar launches of at most SK_MAX_M rows that opt in run
   // gemm_skinny.hpp (the linearised entry's G); the unembed keeps the pingpong
   // kernel so its logits path and fused statistics share one GEMM
@@ -161,16 +166,21 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
 // the activation format of EPI_SPLIT_GELU_ACT's GELU columns.
 template <int EPI, int FMT = ACT_X2F16>
 __device__ __forceinline__ void epi_store(const GemmEpi& ep, size_t orow, int col, float v) {
+  const bool mirror = ep.out0m && orow < (size_t)ep.mirror_rows;
   if constexpr (EPI == EPI_BIAS) {
     ep.out0[orow * ep.ld0 + col] = v;
+    if (mirror) ep.out0m[orow * ep.ld0 + col] = v;
   } else if constexpr (EPI == EPI_SPLIT_GELU) {
-    if (col < ep.n_split)
+    if (col < ep.n_split) {
       ep.out0[orow * ep.ld0 + col] = v;
-    else
+      if (mirror) ep.out0m[orow * ep.ld0 + col] = v;
+    } else {
       ep.out1[orow * ep.ld1 + (col - ep.n_split)] = gelu_erf(v);
+    }
   } else if constexpr (EPI == EPI_SPLIT_GELU_ACT) {
     if (col < ep.n_split) {
       ep.out0[orow * ep.ld0 + col] = v;
+      if (mirror) ep.out0m[orow * ep.ld0 + col] = v;
     } else {
       if (ep.raw && orow < (size_t)ep.raw_rows) ep.raw[orow * ep.ld_raw + (col - ep.n_split)] = v;
       store_act<FMT>(ep.out1h + orow * ep.ld1h + (col - ep.n_split), ep.ps1h, gelu_erf(v), ep.range_flag);

@@ -92,9 +92,11 @@ template <int EPI, int FMT, bool NT = false>
 __device__ __forceinline__ void epi_store4(const GemmEpi& ep, size_t orow, int n0, f32x4 v) {
   if constexpr (EPI == EPI_BIAS) {
     st16<NT>(ep.out0 + orow * ep.ld0 + n0, v);
+    if (ep.out0m && orow < (size_t)ep.mirror_rows) st16<false>(ep.out0m + orow * ep.ld0 + n0, v);
   } else if constexpr (EPI == EPI_SPLIT_GELU_ACT) {
     if (n0 < ep.n_split) {  // n_split % 4 == 0: a group never straddles it
       st16<NT>(ep.out0 + orow * ep.ld0 + n0, v);
+      if (ep.out0m && orow < (size_t)ep.mirror_rows) st16<false>(ep.out0m + orow * ep.ld0 + n0, v);
     } else {
       if (ep.raw && orow < (size_t)ep.raw_rows) st16<false>(ep.raw + orow * ep.ld_raw + (n0 - ep.n_split), v);
       const f32x2 g01 = gelu_erf2(f32x2{v[0], v[1]}), g23 = gelu_erf2(f32x2{v[2], v[3]});

@@ -72,7 +72,8 @@ template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
                              void* __restrict__ y, int ldy, int rows, int d,
-                             float eps, float2* __restrict__ stats) {
+                             float eps, float2* __restrict__ stats, float* __restrict__ copy = nullptr,
+                             int copy_rows = 0) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;
@@ -86,6 +87,12 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
 #pragma unroll
     for (int u = 0; u < LN_REG_F4; ++u)
       if (u < nv) v[u] = xr[lane + 64 * u];
+    if (copy && r < copy_rows) {  // the input row itself (a fused sweep's clean rows -> the trace)
+      float4* cr = (float4*)(copy + (size_t)r * ldx);
+#pragma unroll
+      for (int u = 0; u < LN_REG_F4; ++u)
+        if (u < nv) cr[lane + 64 * u] = v[u];
+    }
 #pragma unroll
     for (int u = 0; u < LN_REG_F4; ++u)
       if (u < nv) s += (v[u].x + v[u].y) + (v[u].z + v[u].w);
@@ -118,6 +125,7 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
   for (int c = lane; c < d4; c += 64) {
     const float4 v = xr[c];
     s += (v.x + v.y) + (v.z + v.w);
+    if (copy && r < copy_rows) ((float4*)(copy + (size_t)r * ldx))[c] = v;
   }
   const float mean = wave_sum(s) / (float)d;
   float ss = 0.f;
