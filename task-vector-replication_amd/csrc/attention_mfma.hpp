@@ -29,6 +29,7 @@
 
 #include "gemm_planar.hpp"
 #include "kernels.hpp"
+#include "split.hpp"
 
 namespace tvr {
 
@@ -302,7 +303,36 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (q0 + li < sd.n) {
+    if constexpr (STAGE) {
+      // z through the wave's staged-Q region (read above): then each lane stores 8 consecutive dims of one
+      // row (one 16-B store per plane), so a row's DH dims leave as one contiguous run per plane
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) *(f4*)(stg + li * DH + 16 * dt + 4 * g) = zt[dt];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      constexpr int C8 = DH / 8;  // 8-dim chunks per row
+      for (int id = lane; id < 16 * C8; id += 64) {
+        const int r = id / C8, c = id - r * C8;
+        if (q0 + r >= sd.n) continue;
+        const float* src = stg + r * DH + 8 * c;
+        const f4 a = *(const f4*)src, b = *(const f4*)(src + 4);
+        const size_t zrow = (size_t)(sd.row0 + q0 + r);
+        const int col = h * DH + 8 * c;
+        if constexpr (FMT != ACT_F32) {
+          const float v8[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+          store_act8<FMT>((uint16_t*)z + zrow * 2 * ldz + col, ldz, v8, flag);
+        } else {
+          *(f4*)((float*)z + zrow * ldz + col) = a;
+          *(f4*)((float*)z + zrow * ldz + col + 4) = b;
+        }
+        float* zd = nullptr;
+        if (zf && !zf_last && zrow < (size_t)zf_rows) zd = zf + zrow * ldzf + col;
+        if (zf && zf_last && q0 + r == sd.n - 1) zd = zf + (size_t)s * ldzf + col;
+        if (zd) {
+          *(f4*)zd = a;
+          *(f4*)(zd + 4) = b;
+        }
+      }
+    } else if (q0 + li < sd.n) {
       const size_t zrow = (size_t)(sd.row0 + q0 + li);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
