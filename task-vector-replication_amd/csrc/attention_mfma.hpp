@@ -55,8 +55,9 @@ constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 // fragments come from LDS instead of 4-B global loads; the fragments are then
 // read from LDS in the MFMA layout.  No block barrier: each wave owns its
 // region and waits for its own DMAs (vmcnt).
-template <int FMT, int DH, int NKT, bool STAGE = false>
-__global__ void __launch_bounds__(64 * ATTM_WAVES, STAGE ? 2 : (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
+// STAGE 2: K and V only (Q loaded directly; 2/3 of the LDS, so 3 blocks per CU).
+template <int FMT, int DH, int NKT, int STAGE = 0>
+__global__ void __launch_bounds__(64 * ATTM_WAVES, STAGE == 1 ? 2 : STAGE == 2 ? 3 : (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
 attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
                       const SeqDesc* __restrict__ seqs, int n_seqs, int n_heads, void* __restrict__ z, int ldz,
                       float* __restrict__ zf, int ldzf, int zf_last, int zf_rows, unsigned* __restrict__ flag,
@@ -68,9 +69,10 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   constexpr bool LONG = NKT == 0;
   constexpr int MAXKT = LONG ? 8 : NKT;
   static_assert(DH % 16 == 0 && DH <= 128 && MAXKT * 16 <= ATT_MAX_T, "d_head / key tiles");
-  static_assert(!STAGE || NKT == 1, "LDS staging: one key tile");
+  static_assert(STAGE == 0 || NKT == 1, "LDS staging: one key tile");
   constexpr int SMAT = 16 * DH;  // floats of one staged [16][DH] matrix
-  __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * 3 * SMAT : 4];
+  constexpr int NMAT = STAGE == 1 ? 3 : 2, KOFF = STAGE == 1 ? SMAT : 0;  // staged matrices; K's offset
+  __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * NMAT * SMAT : 4];
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
   if (pair >= n_seqs * n_heads) return;  // a whole wave; nothing below synchronises
@@ -108,18 +110,18 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     }
   };
 
-  float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * 3 * SMAT : 0);
-  if constexpr (STAGE) {
+  float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * NMAT * SMAT : 0);
+  if constexpr (STAGE != 0) {
     // rows: Q = the query tile's rows (padding repeats the last), K / V = keys 0 .. 15 (clamped to T - 1);
     // instruction i of matrix m moves chunks 64 i + lane = (row, c) of the packed image
 #pragma unroll
-    for (int mat = 0; mat < 3; ++mat) {
+    for (int mat = STAGE == 1 ? 0 : 1; mat < 3; ++mat) {
 #pragma unroll
       for (int i = 0; i < DH / 16; ++i) {
         const int id = i * 64 + lane, row = id / CH, c = id - row * CH;
         const float* src = mat == 0 ? qkv + (size_t)(sd.row0 + min(sd.q0 + row, sd.n - 1)) * ldq
                                     : row_of(min(row, T - 1)) + mat * d;
-        glds16(src + h * DH + 4 * c, stg + mat * SMAT + i * 256);
+        glds16(src + h * DH + 4 * c, stg + (mat - (STAGE == 1 ? 0 : 1)) * SMAT + i * 256);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -128,7 +130,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     // this lane's query column: relative row q0 + li (padding reuses the last row)
     const int qi = min(q0 + li, sd.n - 1);
     float qf[CH];
-    if constexpr (STAGE)
+    if constexpr (STAGE == 1)
       load_chunk(stg + li * DH, sd.p0 + qi, qf);  // T <= 16: one query tile, staged from q0
     else
       load_chunk(qkv + (size_t)(sd.row0 + qi) * ldq + h * DH, sd.p0 + qi, qf);
@@ -218,7 +220,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
       if constexpr (NKT == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float* vr = STAGE ? stg + 2 * SMAT + (4 * g + r) * DH + li
+          const float* vr = STAGE ? stg + KOFF + SMAT + (4 * g + r) * DH + li
                                   : row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
@@ -232,8 +234,8 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         if (kt < nkt) {
           const int kj = min(16 * kt + li, T - 1);
           float kf[CH];
-          if constexpr (STAGE)
-            load_chunk(stg + SMAT + li * DH, kj, kf);  // staged row li = key min(li, T - 1)
+          if constexpr (STAGE != 0)
+            load_chunk(stg + KOFF + li * DH, kj, kf);  // staged row li = key min(li, T - 1)
           else
             load_chunk(row_of(kj) + d + h * DH, kj, kf);
           // two accumulation chains (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
@@ -303,8 +305,8 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (STAGE) {
-      // z through the wave's staged-Q region (read above): then each lane stores 8 consecutive dims of one
+    if constexpr (STAGE != 0) {
+      // z through the wave's first staged region (Q or K: read above): then each lane stores 8 consecutive dims of one
       // row (one 16-B store per plane), so a row's DH dims leave as one contiguous run per plane
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) *(f4*)(stg + li * DH + 16 * dt + 4 * g) = zt[dt];

@@ -20,7 +20,6 @@
 #include <map>
 #include <string>
 #include <tuple>
-#include <unordered_map>
 #include <vector>
 
 #include "tvr.h"
@@ -98,7 +97,8 @@ struct MatW {
   }
 };
 
-// Launch plan of a planar GEMM (plan_pp).
+// Launch plan of a planar GEMM (plan_pp), cached per (M, N, K, format, GELU epilogue, stream-K switch).
+using PlanKey = std::tuple<int, int, int, int, int, int>;
 struct PpPlan {
   int ksplit = 1;    // whole launch
   int tail_base = 0; // > 0: tiles [0, tail_base) plain, the rest split tail_split ways
@@ -148,7 +148,7 @@ struct tvr_model {
   uint16_t* lin_planes = nullptr;  // layer l at (l - 1) * NPL * H * D1 * KP halves
   float* lin_c1 = nullptr;         // [L][D1]
   std::vector<float> lin_scale;    // per layer: X2F16 plane scale (1 for BF16)
-  std::unordered_map<uint64_t, PpPlan> plans;  // plan_pp_cached: GEMM launch plans per shape
+  std::map<PlanKey, PpPlan> plans;  // plan_pp_cached: GEMM launch plans per shape
 };
 
 struct tvr_trace {
@@ -571,9 +571,7 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi) {
 // plan_pp, cached per launch shape on the model (the sweeps repeat their
 // per-layer shapes: the simulation runs once per shape)
 PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi) {
-  const uint64_t key = ((uint64_t)(uint32_t)M << 32) ^ ((uint64_t)(uint32_t)N << 12) ^ ((uint64_t)(uint32_t)K << 3) ^
-                       ((uint64_t)(a_fmt & 3) << 1) ^ (uint64_t)(epi == EPI_SPLIT_GELU_ACT) ^
-                       ((uint64_t)sk_enabled() << 63);
+  const PlanKey key{M, N, K, a_fmt, epi == EPI_SPLIT_GELU_ACT ? 1 : 0, sk_enabled() ? 1 : 0};
   auto it = m->plans.find(key);
   if (it != m->plans.end()) return it->second;
   const PpPlan p = plan_pp(M, N, K, a_fmt, epi);
@@ -882,13 +880,15 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   // key tiles in registers: 1 / 2 / 4 / 8, or 0 = longer than 128 (chunked online softmax)
   const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 0;
   // one key tile: Q / K / V slices staged through LDS by LDS-DMA (TVR_ATT_STAGE=0: direct loads, A/B)
-  const bool stage = env_flag("TVR_ATT_STAGE");
+  const char* se = getenv("TVR_ATT_STAGE");
+  const int stage = se && std::string(se) == "0" ? 0 : se && std::string(se) == "2" ? 2 : 1;
 #define TVR_ATTM(F, DHV, NK, ...)                                                                                   \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK __VA_OPT__(,) __VA_ARGS__>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
                      inv_scale)
 #define TVR_ATTM_NK(F, DHV)                                                                     \
-  if (nkt == 1 && stage) TVR_ATTM(F, DHV, 1, (DHV <= 80));  /* d_head 128: 98 KB per block, not staged */ \
+  if (nkt == 1 && stage == 1) TVR_ATTM(F, DHV, 1, (DHV <= 80 ? 1 : 0)); /* d_head 128: 98 KB, not staged */ \
+  else if (nkt == 1 && stage == 2) TVR_ATTM(F, DHV, 1, (DHV <= 80 ? 2 : 0));                  \
   else if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                       \
   else if (nkt == 2) TVR_ATTM(F, DHV, 2);                                                       \
   else if (nkt == 4) TVR_ATTM(F, DHV, 4);                                                       \
