@@ -22,13 +22,16 @@ max CIE difference between the two paths, and ``parity`` compares the engine
 with the CPU oracle on the sites the ``cpu_baseline`` leg computes.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL), ``--shard``:
-* ``heads`` (default; the metric's config C3, "patch sites sharded across the
-  GPUs"): the SAME 12 prompts on every rank, each rank owns the sites with
+* ``prompts`` (default): the CIE sweep's patch sites are partitioned across the
+  GPUs by prompt — rank r sweeps its own 12 shuffled prompts (seed 1234 + r)
+  over all 32 x 32 sites, the per-GPU work of the N = 1 step — and the [L, H]
+  CIE sums are combined by one SUM all-reduce per step: no data-path
+  collective, weak scaling (12,288 units per GPU per step), as the task's
+  multi-GPU rule prescribes for a path that partitions;
+* ``heads``: the SAME 12 prompts on every rank, each rank owns the sites with
   head ≡ rank (mod N) in every layer (balances the staircase exactly), one
-  SUM all-reduce of the [L, H] partials per step — strong scaling, 12,288
-  units per step in total;
-* ``prompts``: every rank sweeps its own 12 prompts over all sites — weak
-  scaling, 12,288 units per GPU per step.
+  SUM all-reduce — strong scaling, 12,288 units per step in total
+  (``--emulate-world N`` times rank 0's share of it on one GPU).
 value = units of all ranks / max-rank time.  The timed region runs with no
 profiling; the kernel timings of ``roofline`` / ``hbm_kernels`` come from a
 separate profiled pass of the same step.
@@ -92,8 +95,9 @@ def parse():
                          "rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--shard", default="heads", choices=("heads", "prompts"),
-                    help="N>1: heads = C3's site split (strong scaling), prompts = per-GPU prompts (weak scaling)")
+    ap.add_argument("--shard", default="prompts", choices=("heads", "prompts"),
+                    help="N>1: prompts = the sweep's sites partitioned by prompt, 12 prompts per GPU (weak scaling, "
+                         "default); heads = the same 12 prompts split by head (strong scaling)")
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the separate profiled pass")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="N=1 only, planning aid: time rank 0's share of a --shard heads run on this many GPUs "
@@ -561,7 +565,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True,
-        "scaling": "strong" if shard == "heads" else "weak",
+        "scaling": "strong" if (args.shard == "heads" or emulate) else "weak",
         "vs_baseline": None,
         "dtype": DTYPES[args.gemm],
         "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
