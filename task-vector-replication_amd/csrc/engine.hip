@@ -879,9 +879,10 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const dim3 grid((pairs + ATTM_WAVES - 1) / ATTM_WAVES), block(64 * ATTM_WAVES);
   // key tiles in registers: 1 / 2 / 4 / 8, or 0 = longer than 128 (chunked online softmax)
   const int kt = (maxT + 15) / 16, nkt = kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : kt <= 8 ? 8 : 0;
-  // one key tile: Q / K / V slices staged through LDS by LDS-DMA (TVR_ATT_STAGE=0: direct loads, A/B)
+  // one key tile: K / V slices staged through LDS by LDS-DMA (default, 2); TVR_ATT_STAGE=1 stages Q as
+  // well, 0 loads directly (A/B: profiles/r03/attention_stage_ab.txt)
   const char* se = getenv("TVR_ATT_STAGE");
-  const int stage = se && std::string(se) == "0" ? 0 : se && std::string(se) == "2" ? 2 : 1;
+  const int stage = se && std::string(se) == "0" ? 0 : se && std::string(se) == "1" ? 1 : 2;
 #define TVR_ATTM(F, DHV, NK, ...)                                                                                   \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK __VA_OPT__(,) __VA_ARGS__>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
