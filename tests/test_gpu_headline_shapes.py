@@ -23,8 +23,8 @@ extraction (a1), both layer sweeps (a4 accuracy, a5 Δprob), the CIE over every
 Tolerances: fp32 paths as tests/test_gpu_engine.py (1e-4 relative on logits
 and vectors, |Δ| <= 1e-4 max|ref| + 1e-7 on probabilities / CIE, accuracies and
 top-k identical); bf16 at the north star's 2e-2 (extracted vectors and logits
-max-abs relative, the fp32 paths' metric), probabilities and CIE within 5e-2 of the
-largest probability involved (bf16's own rounding), accuracies within 0.1.
+max-abs relative, the fp32 paths' metric), probabilities, Δprob and CIE within 2e-2
+of the largest probability involved, accuracies within 0.1.
 """
 import random
 
@@ -46,10 +46,12 @@ WIDTHS = {
 }
 CASES = [("2.8b", "x2f16"), ("2.8b", "f32"), ("12b", "x2f16"), ("6.9b", "bf16")]
 STD = 0.1
-# bf16: the north star's 2e-2 bar is for extracted vectors; probabilities and CIE
-# carry bf16's own rounding of the GEMM inputs (2^-9 relative) through logits of
-# std ~6 at these weights, measured 2.7e-2 of the largest probability at 6.9B width
-BF16_PROB_TOL = 5e-2
+# bf16: the north star's 2e-2 bar (stated for extracted vectors) applied to the
+# probabilities, Δprob and CIE as well, relative to the largest probability
+# involved: with the attention-score projections on fp16 operands (csrc/split.hpp
+# store_ln4) the 6.9B-width CIE is off by 1.87e-2 of p_max (2.7e-2 when Q / K
+# were bf16, which is what the round-2 bar of 5e-2 covered), Δprob by 4.9e-3
+BF16_PROB_TOL = 2e-2
 _CACHE = {}
 
 
@@ -124,6 +126,9 @@ def test_headline_width_parity(width, gemm):
             pr = torch.softmax(ref.double(), 0)
             pmax = max(pmax, pr.max().item())
             ptol = BF16_PROB_TOL if bf16 else tol
+            if bf16:
+                print(f"bf16 clean prob {i}: err {abs(out['prob'][i].item() - pr[r['answers'][i]].item()):.3e}, "
+                      f"p_max {pr.max().item():.3f}")
             assert abs(out["prob"][i].item() - pr[r["answers"][i]].item()) <= ptol * pr.max().item() + 1e-7
             if not bf16:
                 assert out["topk"][i].tolist() == torch.topk(ref, 5).indices.tolist(), i
@@ -153,7 +158,7 @@ def test_headline_width_parity(width, gemm):
         sums = tvr_amd.experiments.causal_indirect_effect_sums(r["mean"].cuda(), r["prompts"], r["answers"], model)
         cie = sums.cpu().double() / len(r["prompts"])
         err = (cie - r["cie"].double()).abs().max().item()
-        if bf16:  # bf16 rounding of the GEMM inputs on std-6 logits: ~2.7e-2 of p at p = 0.91
+        if bf16:  # bf16 rounding of the GEMM inputs on std-6 logits: 1.87e-2 of p at p = 0.91
             print(f"bf16 CIE: max abs err {err:.3e} = {err / pmax:.3e} of p_max {pmax:.3f}")
             assert err <= BF16_PROB_TOL * pmax, (err, pmax)
         else:

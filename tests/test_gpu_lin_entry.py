@@ -75,8 +75,10 @@ def test_cie_matches_oracle_with_lin_entry(deep, gemm):
     cie_ref = R.calculate_average_causal_indirect_effect(mean_ref, prompts, answers, oracle)
     cie = tvr_amd.calculate_average_causal_indirect_effect(mean_ref.cuda(), prompts, answers, model=model).cpu()
     bound = cie_ref.abs().max().item()
-    tol = 1e-4 if gemm == "x2f16" else 5e-2
-    assert (cie.double() - cie_ref.double()).abs().max().item() <= tol * bound + 1e-7
+    tol = 1e-4 if gemm == "x2f16" else 2e-2  # bf16: the north star's 2e-2
+    err = (cie.double() - cie_ref.double()).abs().max().item()
+    print(f"{gemm}: CIE err {err:.3e} = {err / bound:.3e} of max |CIE| {bound:.3e}")
+    assert err <= tol * bound + 1e-7
     if gemm == "x2f16":  # the highest-effect heads are the same
         assert torch.topk(cie.flatten(), 5).indices.tolist() == torch.topk(cie_ref.flatten(), 5).indices.tolist()
     model._check_range("lin entry test")
@@ -146,7 +148,7 @@ def test_lin_entry_equals_full_entry_gemm(deep, gemm, monkeypatch):
 # oracle's own error against fp64 where that is larger — at 12B width the fp32
 # oracle is off by 4.8e-5 and both engine paths by 0.8-1.0e-4 of 0.54;
 # top-5 heads identical),
-# and the two to each other at the same bar; bf16 at its own (5e-2 of the
+# and the two to each other at the same bar; bf16 at the north star's 2e-2 (of the
 # largest probability, as tests/test_gpu_headline_shapes.py).
 WIDE = [("pythia-2.8b", "x2f16", 4), ("pythia-12b", "x2f16", 10), ("pythia-6.9b", "bf16", 5)]
 
@@ -204,8 +206,10 @@ def test_lin_entry_at_headline_widths(name, gemm, kshot, monkeypatch):
             assert err <= bar, (lin, err, e32, ef, ref.abs().max().item())
             assert torch.topk(one.cpu().flatten(), 5).indices.tolist() == \
                 torch.topk(ref.flatten(), 5).indices.tolist(), lin
-    else:
-        assert (cies["1"] - cies["0"]).abs().max().item() <= 5e-2 * pmax
+    else:  # bf16: the north star's 2e-2 bar, relative to the largest probability involved
+        d = (cies["1"] - cies["0"]).abs().max().item()
+        print(f"{name} bf16: linearised vs full entry {d:.3e} = {d / pmax:.3e} of p_max {pmax:.3f}")
+        assert d <= 2e-2 * pmax
     model._check_range("lin entry headline widths")
 
 
@@ -236,6 +240,8 @@ def test_lin_entry_head_shard_at_headline_widths(name, gemm, kshot, monkeypatch)
     assert big > 1e-3
     other = [h for h in range(cfg.n_heads) if h not in heads]
     assert sums["1"][:, other].abs().max().item() == 0.0
-    bar = 1e-4 * big + 1e-7 if gemm == "x2f16" else 5e-2 * pmax
-    assert (sums["1"] - sums["0"]).abs().max().item() <= bar
+    bar = 1e-4 * big + 1e-7 if gemm == "x2f16" else 2e-2 * pmax
+    d = (sums["1"] - sums["0"]).abs().max().item()
+    print(f"{name} {gemm} head shard: linearised vs full entry {d:.3e} (bar {bar:.3e})")
+    assert d <= bar
     model._check_range("lin entry head shard")
