@@ -700,6 +700,10 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   return TVR_OK;
 }
 
+// TVR_GEMM_BF16: the attention-score columns [0, 2d) of the linearised entry
+// run on fp16 operands when they are whole 256-column tiles (else 0: bf16)
+int lin_qk_cols(const tvr_config& c) { return (2 * c.d_model) % 256 == 0 ? 2 * c.d_model : 0; }
+
 // The linearised entry layer's model constants (lin_entry.hpp) for the
 // current planar mode: per layer l = 1 .. L-2, Wsc = W1[l] W_O[l-1] on the
 // exact-product fp32 MFMA GEMM, its planes (X2F16: per-layer power-of-two
@@ -749,11 +753,12 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
     rc = launch_gemm(EPI_BIAS, m->layers[l].w1, d, ACT_F32, MatW{wt}, d, N, d, d, e, st);
     if (rc != TVR_OK) break;
     float scale = 1.0f;
-    if (fmt == ACT_X2F16) {
+    {  // X2F16: one power-of-two scale from max |Wsc|; BF16: from max |Wsc| over the Q / K rows (fp16 there)
       unsigned hm = 0;
       hipError_t e2 = hipMemsetAsync(d_max, 0, sizeof(unsigned), st);
       if (e2 == hipSuccess) {
-        hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, sc, (size_t)N * d, d_max);
+        const size_t n_abs = fmt == ACT_X2F16 ? (size_t)N * d : (size_t)2 * d * d;
+        hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, st, sc, n_abs, d_max);
         e2 = hipGetLastError();
       }
       if (e2 == hipSuccess) e2 = hipMemcpyAsync(&hm, d_max, sizeof(unsigned), hipMemcpyDeviceToHost, st);
@@ -765,11 +770,15 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
       float v;
       std::memcpy(&v, &hm, sizeof(v));
       scale = x2_weight_scale(v);
+    }
+    if (fmt == ACT_X2F16) {
       hipLaunchKernelGGL(lin_planes_kernel<ACT_X2F16>, dim3(4096), dim3(256), 0, st, sc, N, H, dh, KP, scale,
-                         m->lin_planes + (size_t)(l - 1) * npl * per);
-    } else {
-      hipLaunchKernelGGL(lin_planes_kernel<ACT_BF16>, dim3(4096), dim3(256), 0, st, sc, N, H, dh, KP, 1.0f,
-                         m->lin_planes + (size_t)(l - 1) * npl * per);
+                         m->lin_planes + (size_t)(l - 1) * npl * per, 0);
+    } else {  // fp16 Q / K rows when they fill whole 256-column tiles of lin_entry_kernel (every Pythia but tiny)
+      const int n_qk = lin_qk_cols(c);
+      if (n_qk == 0) scale = 1.0f;
+      hipLaunchKernelGGL(lin_planes_kernel<ACT_BF16>, dim3(4096), dim3(256), 0, st, sc, N, H, dh, KP, scale,
+                         m->lin_planes + (size_t)(l - 1) * npl * per, n_qk);
     }
     m->lin_scale[l] = scale;
     hipLaunchKernelGGL(rowsum_kernel, dim3((N + 3) / 4), dim3(256), 0, st, m->layers[l].w1, N, d,
@@ -2079,9 +2088,8 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     if (fmt == ACT_X2F16)
       hipLaunchKernelGGL(act_rows_kernel<ACT_X2F16>, g, dim3(256), 0, st, vectors, d, vact, n_vectors, d,
                          m->range_flag);
-    else
-      hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, g, dim3(256), 0, st, vectors, d, vact, n_vectors, d,
-                         m->range_flag);
+    else  // bf16 plane + the fp16 plane the Q / K columns of G read (as LayerNorm's store_ln4)
+      hipLaunchKernelGGL(act_rows_bf16_f16_kernel, g, dim3(256), 0, st, vectors, d, vact, n_vectors, d);
     TVR_HIP(hipGetLastError());
   }
   // layer l's block with the linearised entry rows [Rp, Rl) (use_lin[l])
@@ -2103,26 +2111,54 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     eg.ld0 = D1;
     eg.a_rows = (const int32_t*)(base + o_lin_vids) + lin_vid_off[l];
     eg.skinny = 1;
-    int rc = launch_gemm(EPI_BIAS, vact, d, fmt, m->w1[l], d, lin_nv[l], D1, d, eg, st, m);
+    int rc = TVR_OK;
+    const int nqk = fmt == ACT_BF16 && !m->w1qk.empty() ? 2 * d : 0;  // bf16: Q / K columns on fp16 operands
+    if (nqk > 0) {
+      rc = launch_gemm(EPI_BIAS, vact + d, d, ACT_F16, m->w1qk[l], d, lin_nv[l], nqk, d, eg, st, m);
+      GemmEpi e2 = eg;
+      e2.out0 = eg.out0 + nqk;
+      if (rc == TVR_OK)
+        rc = launch_gemm(EPI_BIAS, vact, d, fmt, m->w1[l].rows((size_t)nqk * d), d, lin_nv[l], D1 - nqk, d, e2, st,
+                         m);
+    } else {
+      rc = launch_gemm(EPI_BIAS, vact, d, fmt, m->w1[l], d, lin_nv[l], D1, d, eg, st, m);
+    }
     m->prof = prof;
     TVR_TRY(rc);
     const int npl = fmt == ACT_X2F16 ? 2 : 1, KP = m->lin_kp;
     const size_t per = (size_t)c.n_heads * D1 * KP;
     const uint16_t* wp = m->lin_planes + (size_t)(l - 1) * npl * per;
-    const float acc_scale = fmt == ACT_X2F16 ? 1.0f / (m->lin_scale[l] * X2_ASCALE) : 1.0f;
-    const dim3 g(lin_nmb[l] * ((D1 + 255) / 256));
+    // X2F16: every column tile in one launch; BF16: the Q / K column tiles [0, 2d) on the fp16 rows of the
+    // planes (scale lin_scale[l]), the rest on bf16
+    const int n_ct = (D1 + 255) / 256, ct_qk = fmt == ACT_BF16 ? lin_qk_cols(c) / 256 : 0;
+    float acc_scale = fmt == ACT_X2F16 ? 1.0f / (m->lin_scale[l] * X2_ASCALE) : 1.0f;
+    dim3 g;
+    int ct_base = 0;
 #define TVR_LIN(F, NK)                                                                                             \
   hipLaunchKernelGGL((lin_entry_kernel<F, NK>), g, dim3(LIN_THREADS), 0, st,                                       \
                      (const LinMB*)(base + o_lin_mbs) + lin_mb_off[l], lin_nmb[l], (const LinRow*)(base + o_lin_rows), \
                      wp, per, acc_scale, trace->z + (size_t)(l - 1) * tstride, d, c.d_head, lnstats, a.qkv, raw_h,     \
                      c.d_mlp, (const float*)(base + o_g), m->lin_c1 + (size_t)l * D1, w.b1, D1,                         \
-                     reinterpret_cast<uint16_t*>(a.a2) + d, 2 * m->K2, m->K2, m->range_flag)
+                     reinterpret_cast<uint16_t*>(a.a2) + d, 2 * m->K2, m->K2, m->range_flag, ct_base)
 #define TVR_LIN_K(F)                                                      \
   if (KP == 32) TVR_LIN(F, 1);                                            \
   else if (KP == 64) TVR_LIN(F, 2);                                       \
   else if (KP == 96) TVR_LIN(F, 3);                                       \
   else TVR_LIN(F, 4)
-    if (fmt == ACT_X2F16) { TVR_LIN_K(ACT_X2F16); } else { TVR_LIN_K(ACT_BF16); }
+    if (fmt == ACT_X2F16) {
+      g = dim3(lin_nmb[l] * n_ct);
+      TVR_LIN_K(ACT_X2F16);
+    } else {
+      if (ct_qk > 0) {
+        g = dim3(lin_nmb[l] * ct_qk);
+        acc_scale = 1.0f / m->lin_scale[l];
+        TVR_LIN_K(ACT_F16);
+      }
+      g = dim3(lin_nmb[l] * (n_ct - ct_qk));
+      acc_scale = 1.0f;
+      ct_base = ct_qk;
+      TVR_LIN_K(ACT_BF16);
+    }
 #undef TVR_LIN_K
 #undef TVR_LIN
     TVR_HIP(hipGetLastError());

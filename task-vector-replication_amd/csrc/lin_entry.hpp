@@ -63,10 +63,12 @@ __global__ void rowsum_kernel(const float* __restrict__ w, int n_rows, int k, fl
 
 // Wsc fp32 [N][H dh] -> planes [NPL][H][N][KP] (head-major, k zero-padded to
 // KP): X2F16 two fp16 planes of w * scale (as the model's weight planes),
-// BF16 one bf16 plane.
+// BF16 one plane: bf16, except the attention-score rows n < n_qk (Q, K), which
+// are fp16 of w * scale (the bf16 mode runs those projections on fp16
+// operands, as launch_w1 does for the full entry GEMM).
 template <int FMT>
 __global__ void lin_planes_kernel(const float* __restrict__ s, int N, int H, int dh, int KP, float scale,
-                                  uint16_t* __restrict__ out) {
+                                  uint16_t* __restrict__ out, int n_qk = 0) {
   const size_t n_out = (size_t)H * N * KP;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_out; i += (size_t)gridDim.x * blockDim.x) {
     const int k = (int)(i % KP);
@@ -79,7 +81,7 @@ __global__ void lin_planes_kernel(const float* __restrict__ s, int N, int H, int
       out[i] = __builtin_bit_cast(uint16_t, h0);
       out[n_out + i] = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)h0));
     } else {
-      out[i] = bf16_bits(w);
+      out[i] = n < n_qk ? __builtin_bit_cast(uint16_t, (_Float16)(w * scale)) : bf16_bits(w);
     }
   }
 }
@@ -110,7 +112,8 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
                  const uint16_t* __restrict__ wp, size_t wps, float acc_scale, const float* __restrict__ z, int d,
                  int dh, const float2* __restrict__ stats, float* __restrict__ qkv, const float* __restrict__ raw_h,
                  int d_mlp, const float* __restrict__ G, const float* __restrict__ c1, const float* __restrict__ b1,
-                 int N, uint16_t* __restrict__ out1h, int ld1h, int ps1h, unsigned* __restrict__ range_flag) {
+                 int N, uint16_t* __restrict__ out1h, int ld1h, int ps1h, unsigned* __restrict__ range_flag,
+                 int ct_base = 0) {
   using frag = typename PlanarFmt<FMT>::frag;
   constexpr int KP = 32 * NK;
   __shared__ __attribute__((aligned(16))) float tile[64 * LIN_LDR];
@@ -118,7 +121,7 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
   const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int mbi = work % n_mb, ct = work / n_mb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int col0 = ct * 256, nb = col0 + wave * 64;
+  const int col0 = (ct_base + ct) * 256, nb = col0 + wave * 64;
   const LinMB mb = mbs[mbi];
   const int r16 = lane & 15, g = lane >> 4;
   // per-row combine coefficients, staged while the product runs:
@@ -185,6 +188,8 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
             const _Float16 h0 = (_Float16)s16;
             a0[i][e] = h0;
             a1[i][e] = (_Float16)(s16 - (float)h0);
+          } else if constexpr (FMT == ACT_F16) {  // the bf16 mode's Q / K columns
+            a0[i][e] = (_Float16)v[e];
           } else {
             a0[i][e] = (__bf16)v[e];
           }
@@ -198,6 +203,8 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
           if constexpr (FMT == ACT_X2F16) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[b][j], a1[i], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[b][j], a0[i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[b][j], a0[i], c, 0, 0, 0);
+          } else if constexpr (FMT == ACT_F16) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[b][j], a0[i], c, 0, 0, 0);
           } else {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[b][j], a0[i], c, 0, 0, 0);

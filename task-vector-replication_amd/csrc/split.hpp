@@ -167,6 +167,20 @@ __global__ void act_rows_kernel(const float* __restrict__ a, int lda, uint16_t* 
   }
 }
 
+// fp32 rows a [rows][lda] -> the bf16 activation format with plane 1 holding
+// fp16(a) (as store_ln4: TVR_GEMM_BF16's Q / K products read it): the
+// linearised entry's vectors, K logical columns
+__global__ void act_rows_bf16_f16_kernel(const float* __restrict__ a, int lda, uint16_t* __restrict__ out, int rows,
+                                         int K) {
+  const size_t n = (size_t)rows * K;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / K, c = i % K;
+    const float v = a[r * lda + c];
+    out[r * 2 * K + c] = bf16_bits(v);
+    out[r * 2 * K + K + c] = __builtin_bit_cast(uint16_t, (_Float16)v);
+  }
+}
+
 // W [n] fp32 -> one bf16 plane (TVR_GEMM_BF16 weights, load time)
 __global__ void bf16_plane_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
