@@ -295,14 +295,18 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   const int wave = t >> 6, lane = t & 63;
   const int wr = wave >> 2, wc = wave & 3;
 
-  // ---- staging map: region R (0 A_lo, 1 A_hi, 2 W_lo, 3 W_hi), pieces 2 wave + s
+  // ---- staging map: region R (0 A_lo, 1 A_hi, 2 W_lo, 3 W_hi), pieces 2 wave + s.
+  // The piece geometry is wave-uniform (readfirstlane): the LDS destinations
+  // (M0) are then scalar, so a stage costs one VALU address add per piece
+  // instead of five (add, select, shift, readfirstlane for M0, address).
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
   const uint16_t* src[4][2];
   int dst[4][2];
 #pragma unroll
   for (int R = 0; R < 4; ++R) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int pi = 2 * wave + s;
+      const int pi = 2 * wave_s + s;
       const int plane = pi / PPP, x0 = (pi % PPP) * RPP;  // region row of the piece's first row
       int trow0;                                          // tile row of it
       if (R < 2)

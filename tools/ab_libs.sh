@@ -8,7 +8,7 @@ OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
   for lib in $LA $LB; do
-    n=$(basename $lib .so)_$r
+    n=$(basename $(dirname $lib))_$(basename $lib .so)_$r
     TVR_LIB=$lib timeout -k 10 240 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-f32-leg --extract 0 "$@" \
         > $OUT/$n.json 2> $OUT/$n.err || { tail -5 $OUT/$n.err; exit 1; }
     python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; h=d.get('hbm_kernels') or {}; print(sys.argv[2], d['value'], d['ms_per_step'], r['achieved'], {k: v['achieved_tflops'] for k, v in r['variants'].items()})" $OUT/$n.json $n | tee -a $OUT/summary.txt
