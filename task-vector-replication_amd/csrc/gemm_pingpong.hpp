@@ -138,6 +138,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
   // before the row loops: no global load inside them, only LDS reads and stores.
   bool split8 = false;
   if constexpr (EPI == EPI_SPLIT_GELU_ACT) split8 = col0 >= ep.n_split && Nlim >= 256;
+  float range_mx = 0.f;  // X2F16 GELU planes: the largest scaled magnitude stored, checked once at the end
   const int c8 = (t & 31) * 8, c4 = (t & 63) * 4;
   float b8[8];
   f32x4 b4 = {0.f, 0.f, 0.f, 0.f};
@@ -203,7 +204,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
         }
         if (!NOSTORE || v[0] == 1.2345e-30f)  // NOSTORE (diagnostic): the LDS pass and math without the stores
           store_act8<FMT, PP_NT_STORES>(ep.out1h + (size_t)orow[i] * ep.ld1h + (col0 + c8 - ep.n_split), ep.ps1h, v,
-                                        ep.range_flag);
+                                        ep.range_flag, &range_mx);
       }
     } else if (c4 < Nlim) {
       // 16 rows per thread, in two batches of 8: the residual rows of a batch
@@ -242,6 +243,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
     }
     __syncthreads();
   }
+  if constexpr (EPI == EPI_SPLIT_GELU_ACT && FMT == ACT_X2F16)
+    if (range_mx >= X2_FP16_OVERFLOW && ep.range_flag) atomicOr(ep.range_flag, 1u);
 }
 
 // K must be a multiple of BK (host-checked); any M, N.

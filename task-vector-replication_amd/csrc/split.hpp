@@ -130,9 +130,12 @@ __device__ __forceinline__ void store_ln4(uint16_t* p, int plane, float a, float
   }
 }
 
-// eight consecutive elements (p 16-B aligned): one 16-B store per plane
+// eight consecutive elements (p 16-B aligned): one 16-B store per plane; the
+// X2F16 range check is folded into *mx (the caller raises the flag once, after
+// all its stores: no per-store divergent branch) when mx is given, else done here
 template <int FMT, bool NT = false>
-__device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (&v)[8], unsigned* flag) {
+__device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (&v)[8], unsigned* flag,
+                                           float* mx = nullptr) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   auto st = [](uint16_t* q, u32x4 x) {
     if constexpr (NT)
@@ -147,7 +150,10 @@ __device__ __forceinline__ void store_act8(uint16_t* p, int plane, const float (
     for (int k = 0; k < 4; ++k) split_f16x2(v[2 * k], v[2 * k + 1], lo[k], hi[k], m);
     st(p, u32x4{lo[0], lo[1], lo[2], lo[3]});
     st(p + plane, u32x4{hi[0], hi[1], hi[2], hi[3]});
-    if (m >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
+    if (mx)
+      *mx = fmaxf(*mx, m);
+    else if (m >= X2_FP16_OVERFLOW && flag)
+      atomicOr(flag, 1u);
   } else {
     unsigned w[4];
 #pragma unroll
