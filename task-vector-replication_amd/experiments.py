@@ -142,9 +142,9 @@ def _injection_sweep(model: Model, seqs: List[List[int]], vectors: torch.Tensor,
     outputs, patched outputs [n, len(layers)])."""
     n, layers = len(seqs), list(layers)
     site_layer = np.tile(np.asarray(layers, dtype=np.int32), n)
+    site_vec = np.tile(np.asarray([vec_of_layer(l) for l in layers], dtype=np.int32), n)
     clean, patched = _add_site_outputs(model, seqs, np.repeat(np.arange(n, dtype=np.int32), len(layers)), site_layer,
-                                       np.asarray([vec_of_layer(l) for l in site_layer], dtype=np.int32), vectors,
-                                       targets, topk, shard, clean_outputs)
+                                       site_vec, vectors, targets, topk, shard, clean_outputs)
     return clean, {k: v.view(n, len(layers), *v.shape[1:]) for k, v in patched.items()}
 
 
@@ -156,12 +156,15 @@ def _zero_shot_accuracy(layered_vectors, contexts: Pairs, function_token: str, m
     f = model.to_single_token(function_token)
     seqs = [[0, model.to_single_token(x), f] for x, _ in contexts]
     _, patched = _injection_sweep(model, seqs, vectors, vec_of, range(L), None, 1, shard, clean_outputs=False)
-    top1 = patched["topk"][..., 0].cpu().tolist()
-    hits = [0] * L
-    for (x, y), row in zip(contexts, top1):
-        for i, tid in enumerate(row):
-            hits[i] += model.to_string(tid) == y
-    return [1.0 * h / len(contexts) for h in hits]
+    # top-1 decoded == answer (scratch2.py's to_string comparison), decoding
+    # each distinct token id once instead of once per (prompt, layer)
+    ids, inv = np.unique(patched["topk"][..., 0].cpu().numpy(), return_inverse=True)
+    words = [model.to_string(int(t)) for t in ids]
+    want = {y: i for i, y in enumerate(dict.fromkeys(y for _, y in contexts))}
+    eq = np.array([[w == y for y in want] for w in words], dtype=bool).reshape(len(ids), len(want))
+    col = np.asarray([want[y] for _, y in contexts])
+    hits = eq[inv.reshape(len(contexts), L), col[:, None]].sum(0)
+    return [1.0 * int(h) / len(contexts) for h in hits]
 
 
 @range_checked
