@@ -22,16 +22,16 @@ max CIE difference between the two paths, and ``parity`` compares the engine
 with the CPU oracle on the sites the ``cpu_baseline`` leg computes.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL), ``--shard``:
-* ``prompts`` (default): the CIE sweep's patch sites are partitioned across the
-  GPUs by prompt — rank r sweeps its own 12 shuffled prompts (seed 1234 + r)
-  over all 32 x 32 sites, the per-GPU work of the N = 1 step — and the [L, H]
-  CIE sums are combined by one SUM all-reduce per step: no data-path
-  collective, weak scaling (12,288 units per GPU per step), as the task's
-  multi-GPU rule prescribes for a path that partitions;
-* ``heads``: the SAME 12 prompts on every rank, each rank owns the sites with
-  head ≡ rank (mod N) in every layer (balances the staircase exactly), one
-  SUM all-reduce — strong scaling, 12,288 units per step in total
-  (``--emulate-world N`` times rank 0's share of it on one GPU).
+* ``heads`` (default; BASELINE's C3 "one 32 x 32 sweep sharded across the
+  GPUs"): the SAME 12 prompts on every rank, each rank owns the sites with
+  head ≡ rank (mod N) in every layer (balances the staircase exactly), one SUM
+  all-reduce of the [L, H] CIE sums per step — strong scaling, 12,288 units
+  per step in total whatever N is (``--emulate-world N`` times rank 0's share
+  of it on one GPU).  At N > 1 a short ``weak_prompt_partition`` leg follows:
+  every rank sweeps its own 12 prompts (seed 1234 + rank) over all sites, the
+  weak-scaling figure, reported under its own key and never as ``value``;
+* ``prompts``: that weak form as the headline (12,288 units per GPU per step;
+  no data-path collective, one all-reduce).
 value = units of all ranks / max-rank time.  The timed region runs with no
 profiling; the kernel timings of ``roofline`` / ``hbm_kernels`` come from a
 separate profiled pass of the same step.
@@ -95,9 +95,12 @@ def parse():
                          "rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--shard", default="prompts", choices=("heads", "prompts"),
-                    help="N>1: prompts = the sweep's sites partitioned by prompt, 12 prompts per GPU (weak scaling, "
-                         "default); heads = the same 12 prompts split by head (strong scaling)")
+    ap.add_argument("--shard", default="heads", choices=("heads", "prompts"),
+                    help="N>1: heads = the same 12 prompts split by head mod N (strong scaling: BASELINE's C3, "
+                         "default); prompts = 12 prompts per GPU, sites partitioned by prompt (weak scaling)")
+    ap.add_argument("--weak-leg", dest="weak_leg", action="store_true", default=True,
+                    help="N>1 with --shard heads: also time the prompt-partitioned weak form (own key, not value)")
+    ap.add_argument("--no-weak-leg", dest="weak_leg", action="store_false")
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the separate profiled pass")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="N=1 only, planning aid: time rank 0's share of a --shard heads run on this many GPUs "
@@ -227,6 +230,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def describe_workload(model_name: str, n_layers: int, n_heads: int, prompts: int, kshot: int, T: int, world: int,
+                      shard: str, emulate: int = 0, n_heads_rank: int = 0):
+    """(workload string, scaling label) of the bench line.  The headline at
+    any N is BASELINE's C3: ONE sweep of the same prompts over all L x H sites
+    (strong scaling; at N > 1 the sites split by head mod N).  ``shard ==
+    "prompts"`` at N > 1 is the weak form (prompts per GPU)."""
+    base = f"{model_name} CIE sweep {n_layers}x{n_heads} sites"
+    if emulate:
+        return (f"{model_name} CIE sweep, rank 0's share of a {emulate}-GPU head split ({n_heads_rank} of {n_heads} "
+                f"heads x {n_layers} layers), {prompts} prompts/step, {kshot}-shot, T={T} (planning emulation on "
+                f"one GPU, not the metric)", "strong")
+    if world > 1 and shard == "prompts":
+        return f"{base}, {prompts} prompts/GPU/step, {kshot}-shot, T={T}", "weak"
+    if world > 1:
+        return f"{base}, {prompts} prompts/step, {kshot}-shot, T={T}, sites h = rank (mod {world})", "strong"
+    return f"{base}, {prompts} prompts/step, {kshot}-shot, T={T}", "strong"
+
+
 def _sync_time(fn, reps):
     """fn() run `reps` times between synchronize calls; seconds per call."""
     torch.cuda.synchronize()
@@ -306,7 +327,13 @@ def config_c4(args, dev, n_tasks=3):
     function vector of the top-10 heads (a10) added at every layer over the 50
     zero-shot prompts, top-5 accuracy (a11) — through the sharded entry points
     (one process: the plain functions).  One warm task, then ``n_tasks`` timed
-    (tools/bench_configs.py --configs C4 runs the 20-task suite)."""
+    (tools/bench_configs.py --configs C4 runs the 20-task suite).  Roofline of
+    the CIE sweep (95 % of a task's GEMM work): SURVEY §8d's F_alg per site
+    (T = 18) x CIE sites/s against the bf16 dense peak (``site_frac``), and
+    the bf16 GEMM family's executed TFLOP/s from a separate profiled CIE pass
+    (HIP events on the engine stream), with the committed rocprofv3 PMC
+    summary of the same sweep (profiles/pmc_gemm_bf16.json) when its
+    workload matches."""
     import random
     import tvr_amd
     from tvr_amd import distributed as D
@@ -315,6 +342,7 @@ def config_c4(args, dev, n_tasks=3):
     model = tvr_amd.Model.from_pretrained("pythia-6.9b", device=dev, seed=0, gemm="bf16")
     build_s = time.time() - t0
     arrow = tvr_amd.tasks.ARROW
+    cie_in = {}
 
     def one(ti):
         task = tvr_amd.tasks.synthetic_task(50, model.cfg.d_vocab, seed=100 + ti)
@@ -332,17 +360,46 @@ def config_c4(args, dev, n_tasks=3):
         fv = E.assemble_task_vector(mean, cie, 10, 10)
         acc = D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, task, 5, model)
         torch.cuda.synchronize()
+        cie_in.update(mean=mean, prompts=prompts, answers=answers)
         return time.perf_counter() - t, tc, acc
 
     one(0)  # warm: trace / workspace sizing
     runs = [one(ti) for ti in range(1, n_tasks + 1)]
-    L, H = model.cfg.n_layers, model.cfg.n_heads
+    cfg = model.cfg
+    L, H, d, V = cfg.n_layers, cfg.n_heads, cfg.d_model, cfg.d_vocab
+    # the CIE sweep's roofline: a profiled pass of the last task's sweep
+    model.profile(True)
+    E.calculate_average_causal_indirect_effect(cie_in["mean"], cie_in["prompts"], cie_in["answers"], model=model)
+    torch.cuda.synchronize()
+    st = model.profile_stats()
+    model.profile(False)
+    T = len(model.to_tokens(cie_in["prompts"][0])[0])
+    P_l = 4 * d * d + 2 * d * cfg.d_mlp
+    f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
+    cie_rate = sum(12 * L * H / r[1] for r in runs) / n_tasks
+    peak = PEAKS["bf16"]
+    fam = st["all"]
+    gemm_tf = fam["flops"] / (fam["ms"] * 1e-3) / 1e12 if fam["ms"] else None
+    workload = f"pythia-6.9b CIE sweep {L}x{H} sites, 12 prompts/step, 5-shot, T={T}"
+    pmc, pmc_src = pmc_summary("bf16", workload)
+    variants = {k: round(st[k]["flops"] / (st[k]["ms"] * 1e-3) / 1e12, 2) for k in ("qkv_mlpin", "o_mlpout", "unembed")
+                if st[k]["ms"]}
     del model
     torch.cuda.empty_cache()
     return {"workload": f"pythia-6.9b bf16 FV suite per 50-pair task: extraction 512 x 5-shot, CIE {L}x{H} over 12 "
                         "prompts, top-10-head FV added at every layer over 50 zero-shot prompts (top-5)",
             "gemm": "bf16", "tasks_timed": n_tasks, "s_per_task": round(sum(r[0] for r in runs) / n_tasks, 3),
-            "cie_patched_prompts_per_s": round(sum(12 * L * H / r[1] for r in runs) / n_tasks, 1),
+            "cie_patched_prompts_per_s": round(cie_rate, 1),
+            "cie_roofline": {"workload": workload, "gflop_per_site": round(f_alg / 1e9, 2),
+                             "site_tflops": round(cie_rate * f_alg / 1e12, 2),
+                             "site_frac": round(cie_rate * f_alg / 1e12 / peak, 4), "peak_tflops": peak,
+                             "peak_basis": "bf16 MFMA dense peak (v_mfma_f32_16x16x32_bf16 / _f16, one product)",
+                             "gemm_achieved_tflops": round(gemm_tf, 2) if gemm_tf else None,
+                             "gemm_frac": round(gemm_tf / peak, 4) if gemm_tf else None,
+                             "gemm_variants_tflops": variants,
+                             "mfma_util_rocprof": (pmc.get("mfma") or {}).get("all") if pmc else None,
+                             "traffic_ratio_to_alg": (pmc or {}).get("ratio_hbm_to_alg"),
+                             "pmc_source": pmc_src},
             "fv_top5_acc_by_layer_last_task": runs[-1][2], "model_build_s": round(build_s, 1)}
 
 
@@ -531,16 +588,8 @@ def main():
     fam = st["all"]
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
     T = len(prompts[0])
-    if emulate:
-        workload = (f"{args.model} CIE sweep, rank 0's share of a {emulate}-GPU head split ({len(heads)} of "
-                    f"{cfg.n_heads} heads x {cfg.n_layers} layers), {args.prompts} prompts/step, {args.kshot}-shot, "
-                    f"T={len(prompts[0])} (planning emulation on one GPU, not the metric)")
-    elif shard == "heads" and world > 1:
-        workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/step, "
-                    f"{args.kshot}-shot, T={T}, sites h = rank (mod {world})")
-    else:
-        workload = (f"{args.model} CIE sweep {cfg.n_layers}x{cfg.n_heads} sites, {args.prompts} prompts/GPU/step, "
-                    f"{args.kshot}-shot, T={T}")
+    workload, scaling = describe_workload(args.model, cfg.n_layers, cfg.n_heads, args.prompts, args.kshot, T, world,
+                                          shard, emulate, len(heads))
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     peak = PEAKS[args.gemm]
@@ -570,7 +619,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2),
         "higher_is_better": True,
-        "scaling": "strong" if (args.shard == "heads" or emulate) else "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": DTYPES[args.gemm],
         "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
@@ -632,6 +681,17 @@ def main():
         }
     if emulate:
         out["emulated_world"] = emulate
+    if world > 1 and shard == "heads" and args.weak_leg:
+        # the weak form (own prompts per rank, every site): reported beside the strong headline, never as `value`
+        prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
+        heads = list(range(cfg.n_heads))
+        nw = max(1, min(args.steps, 2))
+        el_w, _ = timed(1, nw, False)
+        out["weak_prompt_partition"] = {
+            "workload": describe_workload(args.model, cfg.n_layers, cfg.n_heads, args.prompts, args.kshot, T, world,
+                                          "prompts")[0],
+            "steps": nw, "value": round(len(prompts) * cfg.n_layers * cfg.n_heads * world * nw / el_w, 2),
+            "unit": "patched prompts/s", "scaling": "weak", "rank_elapsed_s": [round(x, 4) for x in rank_times]}
     if rank == 0 and world == 1 and args.cpu_baseline and not emulate:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
     which = {c for c in args.configs.split(",") if c} if world == 1 and not emulate and args.model == "pythia-2.8b" \

@@ -48,7 +48,8 @@ enum tvr_status {
   TVR_ERR_HIP = -2,         /* HIP runtime failure */
   TVR_ERR_NOMEM = -3,       /* device allocation failed */
   TVR_ERR_UNSUPPORTED = -4, /* shape outside what the kernels handle */
-  TVR_ERR_RANGE = -5        /* a GEMM input exceeded the TVR_GEMM_X2F16 range */
+  TVR_ERR_RANGE = -5,       /* a GEMM input exceeded the TVR_GEMM_X2F16 range */
+  TVR_ERR_INTERNAL = -6     /* an engine invariant failed (a bug: report it) */
 };
 
 /* Patch-site kinds: the declarative replacement for TransformerLens hooks. */

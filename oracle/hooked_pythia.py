@@ -45,67 +45,76 @@ class OracleConfig:
         return self.d_model // self.n_heads
 
 
+def tl_process_block(g: Callable[[str], torch.Tensor], cfg: OracleConfig) -> Dict[str, torch.Tensor]:
+    """One block of TL process_weights_ (every step is per block):
+    fold_ln (biases first, then weights, then centre the read-in weights over
+    d_model) → center_writing_weights → fold_value_biases.  ``g(name)`` gives
+    the block's HF parameter ``name`` (without the ``gpt_neox.layers.{l}.``
+    prefix) as a fresh tensor in the working dtype."""
+    d, H, dh = cfg.d_model, cfg.n_heads, cfg.d_head
+    qkv = g("attention.query_key_value.weight").view(H, 3, dh, d)
+    qkv_b = g("attention.query_key_value.bias").view(H, 3, dh)
+    b = {
+        "W_Q": qkv[:, 0].transpose(1, 2).contiguous(),  # [H, d, dh]
+        "W_K": qkv[:, 1].transpose(1, 2).contiguous(),
+        "W_V": qkv[:, 2].transpose(1, 2).contiguous(),
+        "b_Q": qkv_b[:, 0].clone(), "b_K": qkv_b[:, 1].clone(), "b_V": qkv_b[:, 2].clone(),
+        "W_O": g("attention.dense.weight").T.reshape(H, dh, d).contiguous(),
+        "b_O": g("attention.dense.bias"),
+        "W_in": g("mlp.dense_h_to_4h.weight").T.contiguous(),   # [d, m]
+        "b_in": g("mlp.dense_h_to_4h.bias"),
+        "W_out": g("mlp.dense_4h_to_h.weight").T.contiguous(),  # [m, d]
+        "b_out": g("mlp.dense_4h_to_h.bias"),
+    }
+    ln1_w, ln1_b = g("input_layernorm.weight"), g("input_layernorm.bias")
+    ln2_w, ln2_b = g("post_attention_layernorm.weight"), g("post_attention_layernorm.bias")
+    # --- fold_ln ---
+    for n in "QKV":
+        b["b_" + n] = b["b_" + n] + (b["W_" + n] * ln1_b[None, :, None]).sum(-2)
+        b["W_" + n] = b["W_" + n] * ln1_w[None, :, None]
+        b["W_" + n] = b["W_" + n] - b["W_" + n].mean(-2, keepdim=True)
+    b["b_in"] = b["b_in"] + (b["W_in"] * ln2_b[:, None]).sum(-2)
+    b["W_in"] = b["W_in"] * ln2_w[:, None]
+    b["W_in"] = b["W_in"] - b["W_in"].mean(-2, keepdim=True)
+    # --- center_writing_weights ---
+    b["W_O"] = b["W_O"] - b["W_O"].mean(-1, keepdim=True)
+    b["b_O"] = b["b_O"] - b["b_O"].mean()
+    b["W_out"] = b["W_out"] - b["W_out"].mean(-1, keepdim=True)
+    b["b_out"] = b["b_out"] - b["b_out"].mean()
+    # --- fold_value_biases ---
+    b["b_O"] = b["b_O"] + (b["b_V"][:, :, None] * b["W_O"]).sum([0, 1])
+    b["b_V"] = torch.zeros_like(b["b_V"])
+    return b
+
+
+def tl_process_embed(w_e: torch.Tensor) -> torch.Tensor:
+    """center_writing_weights on W_E [V, d]."""
+    return w_e - w_e.mean(-1, keepdim=True)
+
+
+def tl_process_unembed(embed_out: torch.Tensor, lnf_w: torch.Tensor, lnf_b: torch.Tensor):
+    """HF ``embed_out.weight`` [V, d] → TL (W_U [d, V], b_U [V]): fold_ln of
+    ln_final, then center_unembed.  Pythia has no unembed bias (b_U = 0)."""
+    w_u = embed_out.T.contiguous()
+    b_u = torch.zeros(w_u.shape[1], dtype=w_u.dtype, device=w_u.device)
+    b_u = b_u + (w_u * lnf_b[:, None]).sum(-2)
+    w_u = w_u * lnf_w[:, None]
+    w_u = w_u - w_u.mean(-2, keepdim=True)
+    # --- center_unembed ---
+    w_u = w_u - w_u.mean(-1, keepdim=True)
+    b_u = b_u - b_u.mean()
+    return w_u, b_u
+
+
 def tl_process_weights(sd: Dict[str, torch.Tensor], cfg: OracleConfig, dtype=torch.float32):
     """HF GPT-NeoX state dict → TL state dict, then TL process_weights_:
-    fold_ln → center_writing_weights → center_unembed → fold_value_biases."""
-    d, H, dh = cfg.d_model, cfg.n_heads, cfg.d_head
+    fold_ln → center_writing_weights → center_unembed → fold_value_biases
+    (each step acts per block or on the embed / unembed alone)."""
     g = lambda k: sd[k].to(dtype).clone()  # noqa: E731
-    out = {"W_E": g("gpt_neox.embed_in.weight")}
-    blocks = []
-    for l in range(cfg.n_layers):
-        p = f"gpt_neox.layers.{l}."
-        qkv = g(p + "attention.query_key_value.weight").view(H, 3, dh, d)
-        qkv_b = g(p + "attention.query_key_value.bias").view(H, 3, dh)
-        b = {
-            "W_Q": qkv[:, 0].transpose(1, 2).contiguous(),  # [H, d, dh]
-            "W_K": qkv[:, 1].transpose(1, 2).contiguous(),
-            "W_V": qkv[:, 2].transpose(1, 2).contiguous(),
-            "b_Q": qkv_b[:, 0].clone(), "b_K": qkv_b[:, 1].clone(), "b_V": qkv_b[:, 2].clone(),
-            "W_O": g(p + "attention.dense.weight").T.reshape(H, dh, d).contiguous(),
-            "b_O": g(p + "attention.dense.bias"),
-            "W_in": g(p + "mlp.dense_h_to_4h.weight").T.contiguous(),   # [d, m]
-            "b_in": g(p + "mlp.dense_h_to_4h.bias"),
-            "W_out": g(p + "mlp.dense_4h_to_h.weight").T.contiguous(),  # [m, d]
-            "b_out": g(p + "mlp.dense_4h_to_h.bias"),
-            "ln1_w": g(p + "input_layernorm.weight"), "ln1_b": g(p + "input_layernorm.bias"),
-            "ln2_w": g(p + "post_attention_layernorm.weight"),
-            "ln2_b": g(p + "post_attention_layernorm.bias"),
-        }
-        blocks.append(b)
-    out["W_U"] = g("embed_out.weight").T.contiguous()  # [d, V]
-    out["b_U"] = torch.zeros(cfg.d_vocab, dtype=dtype, device=out["W_U"].device)
-    lnf_w, lnf_b = g("gpt_neox.final_layer_norm.weight"), g("gpt_neox.final_layer_norm.bias")
-
-    # --- fold_ln (biases first, then weights, then centre read-in weights) ---
-    for b in blocks:
-        for n in "QKV":
-            b["b_" + n] = b["b_" + n] + (b["W_" + n] * b["ln1_b"][None, :, None]).sum(-2)
-            b["W_" + n] = b["W_" + n] * b["ln1_w"][None, :, None]
-            b["W_" + n] = b["W_" + n] - b["W_" + n].mean(-2, keepdim=True)
-        b["b_in"] = b["b_in"] + (b["W_in"] * b["ln2_b"][:, None]).sum(-2)
-        b["W_in"] = b["W_in"] * b["ln2_w"][:, None]
-        b["W_in"] = b["W_in"] - b["W_in"].mean(-2, keepdim=True)
-        for k in ("ln1_w", "ln1_b", "ln2_w", "ln2_b"):
-            del b[k]
-    out["b_U"] = out["b_U"] + (out["W_U"] * lnf_b[:, None]).sum(-2)
-    out["W_U"] = out["W_U"] * lnf_w[:, None]
-    out["W_U"] = out["W_U"] - out["W_U"].mean(-2, keepdim=True)
-    # --- center_writing_weights ---
-    out["W_E"] = out["W_E"] - out["W_E"].mean(-1, keepdim=True)
-    for b in blocks:
-        b["W_O"] = b["W_O"] - b["W_O"].mean(-1, keepdim=True)
-        b["b_O"] = b["b_O"] - b["b_O"].mean()
-        b["W_out"] = b["W_out"] - b["W_out"].mean(-1, keepdim=True)
-        b["b_out"] = b["b_out"] - b["b_out"].mean()
-    # --- center_unembed ---
-    out["W_U"] = out["W_U"] - out["W_U"].mean(-1, keepdim=True)
-    out["b_U"] = out["b_U"] - out["b_U"].mean()
-    # --- fold_value_biases ---
-    for b in blocks:
-        b["b_O"] = b["b_O"] + (b["b_V"][:, :, None] * b["W_O"]).sum([0, 1])
-        b["b_V"] = torch.zeros_like(b["b_V"])
-    out["blocks"] = blocks
-    return out
+    blocks = [tl_process_block(lambda n, p=f"gpt_neox.layers.{l}.": g(p + n), cfg) for l in range(cfg.n_layers)]
+    w_u, b_u = tl_process_unembed(g("embed_out.weight"), g("gpt_neox.final_layer_norm.weight"),
+                                  g("gpt_neox.final_layer_norm.bias"))
+    return {"W_E": tl_process_embed(g("gpt_neox.embed_in.weight")), "blocks": blocks, "W_U": w_u, "b_U": b_u}
 
 
 def _cpu(x):

@@ -25,6 +25,7 @@ TVR_ERR_HIP = -2
 TVR_ERR_NOMEM = -3
 TVR_ERR_UNSUPPORTED = -4
 TVR_ERR_RANGE = -5
+TVR_ERR_INTERNAL = -6
 
 # enum tvr_trace_hook
 TRACE_RESID_PRE = 0

@@ -144,6 +144,7 @@ struct tvr_model {
   // l = 1 .. L-2, Wsc = W1[l] W_O[l-1] as weight planes [NPL][H][D1][KP]
   // (head-major, d_head zero-padded to KP) and c1[l] = row sums of W1[l].
   int lin_mode = -1;
+  int lin_failed_mode = -1;  // the planes did not fit in this GEMM mode: the sweeps use the full entry GEMM
   int lin_kp = 0;
   uint16_t* lin_planes = nullptr;  // layer l at (l - 1) * NPL * H * D1 * KP halves
   float* lin_c1 = nullptr;         // [L][D1]
@@ -170,6 +171,7 @@ struct tvr_trace {
   float* p_prob = nullptr;
   int32_t* p_topk = nullptr;
   int p_k = 0;
+  void* p_stream = nullptr;  // the stream of the deferral (its inputs / outputs are ordered on it)
 };
 
 namespace {
@@ -712,6 +714,8 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
   const int fmt = act_fmt(m);
   if (fmt == ACT_F32) return fail(TVR_ERR_INVALID, "lin entry: needs a planar GEMM mode");
   if (m->lin_planes && m->lin_mode == m->gemm_mode) return TVR_OK;
+  if (m->lin_failed_mode == m->gemm_mode)  // remembered: no sync, no allocation attempt per sweep
+    return fail(TVR_ERR_NOMEM, "lin entry: the W1 W_O planes do not fit (earlier attempt)");
   const tvr_config& c = m->cfg;
   const int L = c.n_layers, d = c.d_model, H = c.n_heads, dh = c.d_head, N = m->D1;
   if (L < 3) return fail(TVR_ERR_INVALID, "lin entry: needs >= 3 layers");
@@ -729,17 +733,29 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
     if (sc) (void)hipFree(sc);
     if (d_max) (void)hipFree(d_max);
   };
-  if (hipMalloc(&m->lin_planes, (size_t)(L - 2) * npl * per * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&m->lin_c1, (size_t)L * N * sizeof(float)) != hipSuccess ||
-      hipMalloc(&wt, (size_t)d * d * sizeof(float)) != hipSuccess ||
-      hipMalloc(&sc, (size_t)N * d * sizeof(float)) != hipSuccess ||
-      hipMalloc(&d_max, sizeof(unsigned)) != hipSuccess) {
+  // the split-K partials workspace is regrown on demand: release it for a second attempt
+  for (int attempt = 0;; ++attempt) {
+    if (hipMalloc(&m->lin_planes, (size_t)(L - 2) * npl * per * sizeof(uint16_t)) == hipSuccess &&
+        hipMalloc(&m->lin_c1, (size_t)L * N * sizeof(float)) == hipSuccess &&
+        hipMalloc(&wt, (size_t)d * d * sizeof(float)) == hipSuccess &&
+        hipMalloc(&sc, (size_t)N * d * sizeof(float)) == hipSuccess &&
+        hipMalloc(&d_max, sizeof(unsigned)) == hipSuccess)
+      break;
     (void)hipGetLastError();
     cleanup();
+    wt = sc = nullptr;
+    d_max = nullptr;
     if (m->lin_planes) (void)hipFree(m->lin_planes);
     if (m->lin_c1) (void)hipFree(m->lin_c1);
     m->lin_planes = nullptr;
     m->lin_c1 = nullptr;
+    if (attempt == 0 && m->splitk_ws) {
+      (void)hipFree(m->splitk_ws);
+      m->splitk_ws = nullptr;
+      m->splitk_bytes = 0;
+      continue;
+    }
+    m->lin_failed_mode = m->gemm_mode;
     return fail(TVR_ERR_NOMEM, "lin entry: the W1 W_O planes do not fit");
   }
   m->lin_scale.assign(L, 1.0f);
@@ -1264,6 +1280,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   m->lin_planes = nullptr;
   m->lin_c1 = nullptr;
   m->lin_mode = -1;
+  m->lin_failed_mode = -1;
   m->gemm_mode = TVR_GEMM_F32;
   if (mode == TVR_GEMM_F32) return TVR_OK;
 
@@ -1295,6 +1312,10 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     }
   }
   std::vector<float> scale(mats.size(), 1.0f);  // sized after the Q / K entries: one per matrix
+  // regression guard (415fc26: scale was once sized before the Q / K entries): one size and one scale per
+  // matrix, and the planes of all of them exactly fill the allocation (checked again after the fill)
+  if (scale.size() != mats.size() || sizes.size() != mats.size())
+    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: plane bookkeeping mismatch");
   if (mode == TVR_GEMM_X2F16 || mode == TVR_GEMM_BF16) {
     // one power-of-two scale per matrix from its largest magnitude
     unsigned* d_max = nullptr;
@@ -1343,6 +1364,11 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     }
     TVR_HIP(hipGetLastError());
     p += np * n;
+  }
+  if ((size_t)(p - m->planes) != total) {
+    (void)hipStreamSynchronize(st);
+    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: planes written " + std::to_string(p - m->planes) +
+                                      " != allocated " + std::to_string(total));
   }
   TVR_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(unsigned), st));
   TVR_HIP(hipStreamSynchronize(st));
@@ -1432,10 +1458,14 @@ int tvr_trace_create(tvr_model* m, int32_t max_seqs, int32_t max_tokens, tvr_tra
 
 int tvr_trace_destroy(tvr_trace* t) {
   if (!t) return TVR_OK;
-  // a deferred clean forward still owes its outputs to the caller: run it
-  // (on the null stream, which orders after the caller's blocking streams)
+  // a deferred clean forward still owes its outputs to the caller: run it on
+  // the deferral's stream once everything already queued on any stream (work
+  // sharing the model's workspace included) has finished
   int rc = TVR_OK;
-  if (t->pending) rc = flush_pending(t, nullptr);
+  if (t->pending) {
+    (void)hipDeviceSynchronize();
+    rc = flush_pending(t, t->p_stream);
+  }
   (void)hipDeviceSynchronize();
   if (t->resid) (void)hipFree(t->resid);
   if (t->z) (void)hipFree(t->z);
@@ -1702,6 +1732,7 @@ int tvr_forward_clean_deferred(tvr_model* m, tvr_trace* trace, const int32_t* to
   trace->p_prob = out_prob;
   trace->p_topk = out_topk;
   trace->p_k = topk;
+  trace->p_stream = stream;
   trace->pending = true;
   return TVR_OK;
 }

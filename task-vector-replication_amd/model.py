@@ -111,10 +111,12 @@ class Trace:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            if getattr(self, "_pending_out", None) is not None:
-                self.flush()  # the deferred outputs are owed to the caller (tvr_trace_destroy would also run it)
-            self._lib.tvr_trace_destroy(h)
-            self._h = None
+            try:
+                if getattr(self, "_pending_out", None) is not None:
+                    self.flush()  # the deferred outputs are owed to the caller (tvr_trace_destroy would also run it)
+            finally:  # the device buffers are released even if the flush raised
+                self._lib.tvr_trace_destroy(h)
+                self._h = None
 
 
 # Matrix-core path of the GEMMs (Model.set_gemm): the fp32-accurate 2-plane

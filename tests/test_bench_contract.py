@@ -71,3 +71,27 @@ def test_gpus_flag_launches_ranks_itself():
     out = lines[0]
     assert out["n_gpus"] == 2 and out["launch_check"]
     assert len(out["rank_elapsed_s"]) == 2 and out["max_elapsed_s"] == max(out["rank_elapsed_s"])
+
+
+def test_headline_workload_is_the_strong_c3_sweep():
+    """VERDICT r3 / ADVICE r3: the N > 1 headline is BASELINE's C3 — ONE 12-prompt
+    32 x 32 sweep split by head across the ranks (strong scaling), the default;
+    the prompt-partitioned weak form is opt-in (--shard prompts) or a side leg."""
+    import sys
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py"]
+        assert bench.parse().shard == "heads"
+    finally:
+        sys.argv = argv
+    for world in (1, 2, 8):
+        w, scaling = bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, world, "heads")
+        assert scaling == "strong"
+        assert w.startswith("pythia-2.8b CIE sweep 32x32 sites, 12 prompts/step, 4-shot, T=15")
+        if world > 1:
+            assert w.endswith(f"sites h = rank (mod {world})")
+    w, scaling = bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 8, "prompts")
+    assert scaling == "weak" and "prompts/GPU/step" in w
+    # N = 1: the same string whichever --shard was given (the PMC summaries key on it)
+    assert bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 1, "prompts") == \
+        bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 1, "heads")

@@ -1,0 +1,103 @@
+"""CPU: the layer-streamed fp64 oracle (oracle/streamed_pythia.py) equals the
+whole-model hooked oracle running the reference's loops
+(oracle/reference_experiments.py, scratch2.py:81-100,171-197,292-314) on the
+same seeded weights, to fp64 reassociation (1e-12).  The full-depth GPU tests
+(tests/test_gpu_full_depth.py) use the streamed form at 6.9B / 12B."""
+import random
+
+import pytest
+import torch
+
+import tvr_amd
+from conftest import TINY_STD, make_oracle
+from oracle import reference_experiments as R
+from oracle.streamed_pythia import StreamedPythiaOracle
+
+from conftest import oracle_config
+
+ARROW = tvr_amd.tasks.ARROW
+
+
+@pytest.fixture(scope="module")
+def pair():
+    cfg = tvr_amd.get_config("tiny").with_(n_layers=3)
+    shapes = tvr_amd.weights.hf_param_shapes(cfg)
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 5, "cpu", TINY_STD) for n, s in shapes.items()}
+    tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
+    calls = []
+
+    def get_raw(name):
+        calls.append(name)
+        return sd[name].clone()
+    streamed = StreamedPythiaOracle(oracle_config(cfg), get_raw)
+    return cfg, tok, make_oracle(cfg, sd, tok, torch.float64), streamed, calls
+
+
+def rel(a, b):
+    return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-300)).item()
+
+
+def test_weights_are_streamed_one_block_at_a_time(pair):
+    cfg, _, _, streamed, calls = pair
+    n0 = len(calls)
+    streamed.block(1)
+    streamed.block(1)  # cached
+    assert len(calls) - n0 == 12  # the block's 12 HF parameters, once
+    assert all(c.startswith("gpt_neox.layers.1.") for c in calls[n0:])
+
+
+def test_clean_logits_equal_hooked_oracle(pair):
+    cfg, tok, full, streamed, _ = pair
+    g = random.Random(0)
+    seqs = [[0] + [g.randrange(1, cfg.d_vocab) for _ in range(T - 1)] for T in (5, 9, 9, 14)]
+    got = streamed.last_logits(seqs)
+    for s, row in zip(seqs, got):
+        assert rel(row, full.forward(torch.tensor([s]))[0, -1]) < 1e-12
+
+
+def test_mean_activation_equals_reference_loop(pair):
+    cfg, tok, full, streamed, _ = pair
+    random.seed(7)
+    want = R.generate_mean_activation(list(tvr_amd.tasks.letter_to_caps), ARROW, ",", full, 12, 4)
+
+    class _M:
+        pass
+    m = _M()
+    m.cfg, m.to_single_token, m.tokenizer = cfg, full.to_single_token, tok
+    random.seed(7)
+    prompts = tvr_amd.prompts.sample_icl_prompts(m, list(tvr_amd.tasks.letter_to_caps), ARROW, ",", 12, 4)
+    assert rel(streamed.mean_activation(prompts), want) < 1e-12
+
+
+def test_cie_equals_reference_loop(pair):
+    cfg, tok, full, streamed, _ = pair
+    g = torch.Generator().manual_seed(3)
+    mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g, dtype=torch.float64)
+    r = random.Random(1)
+    prompts = [[0] + [r.randrange(1, cfg.d_vocab) for _ in range(10)] for _ in range(3)]
+    answers = [int(full.forward(torch.tensor([p]))[0, -1].argmax()) for p in prompts]
+    want = R.calculate_average_causal_indirect_effect(mean, prompts, [[a] for a in answers], full)
+    got = streamed.cie(mean, prompts, answers)
+    assert (got - want).abs().max().item() <= 1e-12 * want.abs().max().item()
+    assert want.abs().max().item() > 1e-3
+    sub = streamed.cie(mean, prompts, answers, layers=[0, 2], heads=[1, 3])
+    mask = torch.zeros_like(sub, dtype=torch.bool)
+    mask[torch.tensor([0, 2])[:, None], torch.tensor([1, 3])[None, :]] = True
+    assert (sub[mask] - want[mask]).abs().max().item() <= 1e-12 * want.abs().max().item()
+    assert sub[~mask].abs().max().item() == 0.0
+
+
+def test_added_vector_topk_equals_reference_hook(pair):
+    cfg, tok, full, streamed, _ = pair
+    r = random.Random(2)
+    seqs = [[0, r.randrange(1, cfg.d_vocab), r.randrange(1, cfg.d_vocab)] for _ in range(6)]
+    vec = torch.randn(cfg.d_model, generator=torch.Generator().manual_seed(4), dtype=torch.float64) * 3
+    for layer in (0, 2):
+        got = streamed.added_topk(seqs, layer, vec, 5)
+        for s, row in zip(seqs, got):
+            ref = full.run_with_hooks(torch.tensor([s]), fwd_hooks=[(f"blocks.{layer}.hook_attn_out",
+                                      lambda hv, hook: R.layer_addition_hook(hv, hook, vec))])[0, -1]
+            assert row.tolist() == torch.topk(ref, 5).indices.tolist()
+    clean = streamed.added_topk(seqs, 0, None, 3)
+    for s, row in zip(seqs, clean):
+        assert row.tolist() == torch.topk(full.forward(torch.tensor([s]))[0, -1], 3).indices.tolist()
