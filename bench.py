@@ -22,12 +22,15 @@ max CIE difference between the two paths, and ``parity`` compares the engine
 with the CPU oracle on the sites the ``cpu_baseline`` leg computes.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL), ``--shard``:
-* ``heads`` (default; BASELINE's C3 "one 32 x 32 sweep sharded across the
-  GPUs"): the SAME 12 prompts on every rank, each rank owns the sites with
-  head ≡ rank (mod N) in every layer (balances the staircase exactly), one SUM
-  all-reduce of the [L, H] CIE sums per step — strong scaling, 12,288 units
-  per step in total whatever N is (``--emulate-world N`` times rank 0's share
-  of it on one GPU).  At N > 1 a short ``weak_prompt_partition`` leg follows:
+* ``sites`` (default; BASELINE's C3 "one 32 x 32 sweep sharded across the
+  GPUs"): the SAME 12 prompts on every rank, each rank owns a balanced block
+  of (layer, head) sites (distributed.balanced_site_shard: whole layer pairs
+  (l, L-1-l), every pair the same staircase work; at N = 8 on 2.8B, 2 pairs =
+  4 whole layers per rank), one SUM all-reduce of the [L, H] CIE sums per
+  step — strong scaling, 12,288 units per step in total whatever N is
+  (``--emulate-world N`` times rank 0's share of it on one GPU);
+  ``heads`` is the round-3 split (head ≡ rank mod N in every layer), kept for
+  A/B.  At N > 1 a short ``weak_prompt_partition`` leg follows:
   every rank sweeps its own 12 prompts (seed 1234 + rank) over all sites, the
   weak-scaling figure, reported under its own key and never as ``value``;
 * ``prompts``: that weak form as the headline (12,288 units per GPU per step;
@@ -95,16 +98,17 @@ def parse():
                          "rocprof averages == bench averages)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--shard", default="heads", choices=("heads", "prompts"),
-                    help="N>1: heads = the same 12 prompts split by head mod N (strong scaling: BASELINE's C3, "
-                         "default); prompts = 12 prompts per GPU, sites partitioned by prompt (weak scaling)")
+    ap.add_argument("--shard", default="sites", choices=("sites", "heads", "prompts"),
+                    help="N>1: sites = the same 12 prompts, (layer, head) sites in balanced layer-pair blocks per "
+                         "rank (strong scaling: BASELINE's C3, default); heads = the same prompts split by head mod N "
+                         "(round-3 form); prompts = 12 prompts per GPU, sites partitioned by prompt (weak scaling)")
     ap.add_argument("--weak-leg", dest="weak_leg", action="store_true", default=True,
-                    help="N>1 with --shard heads: also time the prompt-partitioned weak form (own key, not value)")
+                    help="N>1 with a strong split: also time the prompt-partitioned weak form (own key, not value)")
     ap.add_argument("--no-weak-leg", dest="weak_leg", action="store_false")
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the separate profiled pass")
     ap.add_argument("--emulate-world", type=int, default=0,
-                    help="N=1 only, planning aid: time rank 0's share of a --shard heads run on this many GPUs "
-                         "(heads = 0 mod G) on this one GPU; value = the units of that share / its time")
+                    help="N=1 only, planning aid: time rank 0's share of a strong-split run (--shard sites / heads) "
+                         "on this many GPUs on this one GPU; value = the units of that share / its time")
     ap.add_argument("--gemm", default="x2f16", choices=("x2f16", "x3bf16", "f32", "bf16"),
                     help="matrix-core path of the GEMMs (x2f16 / x3bf16 / f32 fp32-accurate; bf16 is the "
                          "north star's bf16 configuration, not the fp32 headline)")
@@ -230,21 +234,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+SPLITS = {"sites": "sites in balanced layer-pair blocks per rank", "heads": "sites h = rank (mod {n})"}
+
+
 def describe_workload(model_name: str, n_layers: int, n_heads: int, prompts: int, kshot: int, T: int, world: int,
-                      shard: str, emulate: int = 0, n_heads_rank: int = 0):
+                      shard: str, emulate: int = 0, n_sites_rank: int = 0):
     """(workload string, scaling label) of the bench line.  The headline at
     any N is BASELINE's C3: ONE sweep of the same prompts over all L x H sites
-    (strong scaling; at N > 1 the sites split by head mod N).  ``shard ==
-    "prompts"`` at N > 1 is the weak form (prompts per GPU)."""
+    (strong scaling; at N > 1 the sites split across the ranks, ``sites`` or
+    ``heads``).  ``shard == "prompts"`` at N > 1 is the weak form (prompts per
+    GPU)."""
     base = f"{model_name} CIE sweep {n_layers}x{n_heads} sites"
     if emulate:
-        return (f"{model_name} CIE sweep, rank 0's share of a {emulate}-GPU head split ({n_heads_rank} of {n_heads} "
-                f"heads x {n_layers} layers), {prompts} prompts/step, {kshot}-shot, T={T} (planning emulation on "
-                f"one GPU, not the metric)", "strong")
+        return (f"{model_name} CIE sweep, rank 0's share of a {emulate}-GPU split "
+                f"({SPLITS.get(shard, shard).format(n=emulate)}: {n_sites_rank} of {n_layers * n_heads} sites), "
+                f"{prompts} prompts/step, {kshot}-shot, T={T} (planning emulation on one GPU, not the metric)",
+                "strong")
     if world > 1 and shard == "prompts":
         return f"{base}, {prompts} prompts/GPU/step, {kshot}-shot, T={T}", "weak"
     if world > 1:
-        return f"{base}, {prompts} prompts/step, {kshot}-shot, T={T}, sites h = rank (mod {world})", "strong"
+        return f"{base}, {prompts} prompts/step, {kshot}-shot, T={T}, {SPLITS[shard].format(n=world)}", "strong"
     return f"{base}, {prompts} prompts/step, {kshot}-shot, T={T}", "strong"
 
 
@@ -354,7 +363,7 @@ def config_c4(args, dev, n_tasks=3):
         prompts, answers = E.generate_shuffled_prompts(task, model, 12, 5, arrow)
         torch.cuda.synchronize()
         tc = time.perf_counter()
-        cie = D.cie_heads_sharded(mean, prompts, answers, model)
+        cie = D.cie_sharded(mean, prompts, answers, model)
         torch.cuda.synchronize()
         tc = time.perf_counter() - tc
         fv = E.assemble_task_vector(mean, cie, 10, 10)
@@ -494,7 +503,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     import tvr_amd
-    from tvr_amd.distributed import strided_shard
+    from tvr_amd.distributed import balanced_site_shard, strided_shard
     from tvr_amd.experiments import causal_indirect_effect_sums, sum_last_z
 
     cfg = tvr_amd.get_config(args.model)
@@ -526,20 +535,25 @@ def main():
         g = torch.Generator(device=dev).manual_seed(4321)
         mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
 
-    shard = args.shard if world > 1 else "heads"
     emulate = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
-    if shard == "heads":  # C3: the same prompts everywhere, sites with head = rank (mod world)
+    shard = args.shard if (world > 1 or emulate) else "sites"
+    if emulate and shard == "prompts":
+        raise SystemExit("--emulate-world times a strong split: --shard sites or heads")
+    everything = [(l, h) for l in range(cfg.n_layers) for h in range(cfg.n_heads)]
+    if shard in ("sites", "heads"):  # C3: the same prompts everywhere, this rank's share of the sites
         prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234)
-        heads = strided_shard(cfg.n_heads, rank, emulate or world)
-        units_total = len(prompts) * cfg.n_layers * (len(heads) if emulate else cfg.n_heads)
+        n_split = emulate or world
+        sites = (balanced_site_shard(cfg.n_layers, cfg.n_heads, rank, n_split) if shard == "sites" else
+                 [(l, h) for l in range(cfg.n_layers) for h in strided_shard(cfg.n_heads, rank, n_split)])
+        units_total = len(prompts) * (len(sites) if emulate else cfg.n_layers * cfg.n_heads)
     else:  # weak scaling: per-rank prompts, every site
         prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
-        heads = list(range(cfg.n_heads))
+        sites = everything
         units_total = len(prompts) * cfg.n_layers * cfg.n_heads * world
-    units_rank = len(prompts) * cfg.n_layers * len(heads)
+    units_rank = len(prompts) * len(sites)
 
     def step():
-        cie = causal_indirect_effect_sums(mean, prompts, answers, model, heads=heads)
+        cie = causal_indirect_effect_sums(mean, prompts, answers, model, sites=sites)
         if world > 1:
             dist.all_reduce(cie)
         return cie
@@ -589,7 +603,7 @@ def main():
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12
     T = len(prompts[0])
     workload, scaling = describe_workload(args.model, cfg.n_layers, cfg.n_heads, args.prompts, args.kshot, T, world,
-                                          shard, emulate, len(heads))
+                                          shard, emulate, len(sites))
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     peak = PEAKS[args.gemm]
@@ -607,8 +621,8 @@ def main():
                               "alg_bytes_per_launch": round(v["bytes"] / v["launches"]),
                               "share_of_gemm_time": round(v["ms"] / fam["ms"], 4)}
     parallelism = ("single GPU" if world == 1 else
-                   f"sites sharded by head mod {world} (same {args.prompts} prompts on every GPU), weights replicated, "
-                   f"1 all-reduce of [L,H] per step" if shard == "heads" else
+                   f"{SPLITS[shard].format(n=world)} (same {args.prompts} prompts on every GPU), weights replicated, "
+                   f"1 all-reduce of [L,H] per step" if shard in SPLITS else
                    f"prompt-sharded x{world}, weights replicated, 1 all-reduce of [L,H] per step")
     out = {
         "metric": METRIC,
@@ -681,10 +695,10 @@ def main():
         }
     if emulate:
         out["emulated_world"] = emulate
-    if world > 1 and shard == "heads" and args.weak_leg:
+    if world > 1 and shard in SPLITS and args.weak_leg:
         # the weak form (own prompts per rank, every site): reported beside the strong headline, never as `value`
         prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234 + rank)
-        heads = list(range(cfg.n_heads))
+        sites = everything
         nw = max(1, min(args.steps, 2))
         el_w, _ = timed(1, nw, False)
         out["weak_prompt_partition"] = {

@@ -6,9 +6,15 @@ data-path communication and ONE collective at the end; the
 model is replicated per GPU (2.8B fp32 11 GB, 12B 47 GB << 288 GB):
 
 * CIE (scratch2.py:181-194): every rank recomputes the clean run of the
-  prompts and owns the sites with head ≡ rank (mod world) in every layer —
-  this balances the staircase exactly, since each layer keeps H/world heads
-  per rank — then one SUM all-reduce of the [L, H] partial sums (4-6 KB).
+  prompts and owns a balanced block of (layer, head) sites
+  (``balanced_site_shard``): the staircase work of a site at layer l is the
+  L - 1 - l blocks after it, so the layer pairs (l, L-1-l) all weigh the same;
+  whole pairs are dealt round-robin and the pairs left over (and the middle
+  layer of an odd L) are split by head (h = rank mod world).  Exact balance
+  whenever world divides H, and each rank's sites fill whole layers, so its
+  staircase GEMMs keep the single-GPU row counts (large M, whole 256-row
+  tiles) instead of 1/world of them at every layer — then one SUM all-reduce
+  of the [L, H] partial sums (4-6 KB).
 * Extraction (scratch2.py:87-98): prompts split contiguously, local Σ z at
   the last position, one SUM all-reduce of [L, d] fp32 (z form: 0.33 MB for
   2.8B), divide by the global count, project to the hook_result form.
@@ -97,16 +103,29 @@ def sharded_site_outputs(n_sites: int, local_fn: Callable[[Sequence[int]], torch
     return shard.gather(local_fn(shard.select(n_sites)), n_sites)
 
 
+def balanced_site_shard(n_layers: int, n_heads: int, rank: int, size: int) -> List[Tuple[int, int]]:
+    """The CIE sites (layer, head) of ``rank``: layer pairs (l, L-1-l) dealt
+    round-robin as whole pairs (every head), the remaining pairs and an odd
+    L's middle layer split by head (h = rank mod size).  Every site exactly
+    once over the ranks; equal staircase work per rank when size | H."""
+    pairs = [(l, n_layers - 1 - l) for l in range(n_layers // 2)]
+    whole = len(pairs) // size
+    out = [(l, h) for p in range(whole * size) if p % size == rank for l in pairs[p] for h in range(n_heads)]
+    rest = [l for p in pairs[whole * size:] for l in p] + ([n_layers // 2] if n_layers % 2 else [])
+    out += [(l, h) for l in rest for h in strided_shard(n_heads, rank, size)]
+    return sorted(out)
+
+
 def sharded_cie(n_layers: int, n_heads: int, n_prompts: int,
-                local_fn: Callable[[Sequence[int]], torch.Tensor], group=None) -> torch.Tensor:
-    """CIE averaged over ``n_prompts`` with heads sharded round-robin.
-    ``local_fn(heads)`` returns Σ_prompts Δp as [L, H] with zeros outside
-    ``heads``."""
+                local_fn: Callable[[Sequence[Tuple[int, int]]], torch.Tensor], zeros: Callable[[], torch.Tensor],
+                group=None) -> torch.Tensor:
+    """CIE averaged over ``n_prompts`` with the sites split by
+    ``balanced_site_shard``.  ``local_fn(sites)`` returns Σ_prompts Δp as
+    [L, H] with zeros outside ``sites``; ``zeros()`` is a rank's empty share."""
     rank, size = world(group)
-    if size > n_heads:  # checked on every rank before any collective: no rank is left waiting in the all-reduce
-        raise ValueError("every rank needs at least one head (world size > n_heads)")
-    heads = strided_shard(n_heads, rank, size)
-    return all_reduce_sum(local_fn(heads).clone(), group) / n_prompts
+    sites = balanced_site_shard(n_layers, n_heads, rank, size)
+    part = local_fn(sites).clone() if sites else zeros()
+    return all_reduce_sum(part, group) / n_prompts
 
 
 def sharded_mean_activation(prompts: Sequence[Sequence[int]],
@@ -124,11 +143,12 @@ def sharded_mean_activation(prompts: Sequence[Sequence[int]],
 
 
 # ------------------------------------------------------------ engine entry points
-def cie_heads_sharded(mean_head_activations, scrambled_prompts, prompt_answers, model, group=None) -> torch.Tensor:
+def cie_sharded(mean_head_activations, scrambled_prompts, prompt_answers, model, group=None) -> torch.Tensor:
     """``calculate_average_causal_indirect_effect`` (scratch2.py:171-197) on
-    this rank's GPU with heads sharded across the process group.  Accepts the
-    reference's forms: string prompts (BOS prepended) or token ids, answers as
-    token-id lists (first token, B3) or ints."""
+    this rank's GPU with the (layer, head) sites split across the process
+    group (``balanced_site_shard``).  Accepts the reference's forms: string
+    prompts (BOS prepended) or token ids, answers as token-id lists (first
+    token, B3) or ints."""
     from .experiments import causal_indirect_effect_sums, normalize_cie_inputs
     cfg = model.cfg
     if tuple(mean_head_activations.shape) != (cfg.n_layers, cfg.n_heads, cfg.d_model):
@@ -137,8 +157,12 @@ def cie_heads_sharded(mean_head_activations, scrambled_prompts, prompt_answers, 
         raise ValueError("Prompt answers must be of the same length as scrambled prompts")
     prompts, answers = normalize_cie_inputs(model, scrambled_prompts, prompt_answers)
     return sharded_cie(cfg.n_layers, cfg.n_heads, len(prompts),
-                       lambda heads: causal_indirect_effect_sums(mean_head_activations, prompts, answers,
-                                                                 model, heads=heads), group)
+                       lambda sites: causal_indirect_effect_sums(mean_head_activations, prompts, answers,
+                                                                 model, sites=sites),
+                       lambda: torch.zeros(cfg.n_layers, cfg.n_heads, device=model.device), group)
+
+
+cie_heads_sharded = cie_sharded  # the round-3 name
 
 
 def mean_activation_sharded(prompts, model, group=None) -> torch.Tensor:

@@ -212,17 +212,27 @@ def normalize_cie_inputs(model: Model, scrambled_prompts, prompt_answers):
 def causal_indirect_effect_sums(mean_head_activations: torch.Tensor, prompts: Sequence[Sequence[int]],
                                 answers: Sequence[int], model: Model,
                                 layers: Optional[Sequence[int]] = None,
-                                heads: Optional[Sequence[int]] = None) -> torch.Tensor:
+                                heads: Optional[Sequence[int]] = None,
+                                sites: Optional[Sequence[Tuple[int, int]]] = None) -> torch.Tensor:
     """Σ over prompts of p_patched(answer) − p_clean(answer) for every
-    (layer, head) site, [n_layers, n_heads] (zeros outside ``layers``/``heads``).
+    (layer, head) site, [n_layers, n_heads] (zeros outside ``layers``/``heads``,
+    or outside the explicit (layer, head) list ``sites``).
     ``prompts`` are token ids (BOS included); one clean forward + one
     staircase sweep per launch-sized group of prompts."""
     cfg = model.cfg
     L, H = cfg.n_layers, cfg.n_heads
-    layers = list(range(L)) if layers is None else list(layers)
-    heads = list(range(H)) if heads is None else list(heads)
-    grid_l = np.repeat(np.asarray(layers, dtype=np.int32), len(heads))
-    grid_h = np.tile(np.asarray(heads, dtype=np.int32), len(layers))
+    if sites is not None:
+        if layers is not None or heads is not None:
+            raise ValueError("give either sites or layers / heads")
+        sl = np.asarray(sites, dtype=np.int32).reshape(-1, 2)
+        if sl.size and (sl[:, 0].min() < 0 or sl[:, 0].max() >= L or sl[:, 1].min() < 0 or sl[:, 1].max() >= H):
+            raise ValueError("site (layer, head) out of range")
+        grid_l, grid_h = sl[:, 0].copy(), sl[:, 1].copy()
+    else:
+        layers = list(range(L)) if layers is None else list(layers)
+        heads = list(range(H)) if heads is None else list(heads)
+        grid_l = np.repeat(np.asarray(layers, dtype=np.int32), len(heads))
+        grid_h = np.tile(np.asarray(heads, dtype=np.int32), len(layers))
     per_prompt = grid_l.size
     vectors = mean_head_activations.to(model.device, torch.float32).reshape(L * H, cfg.d_model).contiguous()
     out = torch.zeros(L, H, device=model.device)

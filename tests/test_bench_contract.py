@@ -81,15 +81,17 @@ def test_headline_workload_is_the_strong_c3_sweep():
     argv = sys.argv
     try:
         sys.argv = ["bench.py"]
-        assert bench.parse().shard == "heads"
+        assert bench.parse().shard == "sites"
     finally:
         sys.argv = argv
     for world in (1, 2, 8):
-        w, scaling = bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, world, "heads")
-        assert scaling == "strong"
-        assert w.startswith("pythia-2.8b CIE sweep 32x32 sites, 12 prompts/step, 4-shot, T=15")
-        if world > 1:
-            assert w.endswith(f"sites h = rank (mod {world})")
+        for shard in ("sites", "heads"):
+            w, scaling = bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, world, shard)
+            assert scaling == "strong"
+            assert w.startswith("pythia-2.8b CIE sweep 32x32 sites, 12 prompts/step, 4-shot, T=15")
+            if world > 1:
+                assert w.endswith("sites in balanced layer-pair blocks per rank" if shard == "sites" else
+                                  f"sites h = rank (mod {world})")
     w, scaling = bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 8, "prompts")
     assert scaling == "weak" and "prompts/GPU/step" in w
     # N = 1: the same string whichever --shard was given (the PMC summaries key on it)

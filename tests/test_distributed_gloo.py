@@ -1,8 +1,8 @@
 """CPU, multi-process (gloo): the multi-GPU partition + reduction logic of
 distributed.py, with the oracle standing in for each rank's GPU sweep.
 
-* head-sharded CIE (head ≡ rank mod world, one SUM all-reduce) == the full
-  single-process oracle CIE;
+* site-sharded CIE (balanced layer-pair blocks, one SUM all-reduce) == the
+  full single-process oracle CIE;
 * prompt-sharded mean extraction (contiguous split, SUM all-reduce, one
   division by the global count) == the unsharded mean.
 """
@@ -39,17 +39,21 @@ def _worker(rank, world, port, q):
         prompts = [[0, 5, 1, 9, 44, 1, 7], [0, 3, 1, 8, 1, 12, 19, 1, 6]]
         answers = [[9], [12]]
 
-        def local(heads):
-            return R.calculate_average_causal_indirect_effect(mean, prompts, answers, oracle,
-                                                              heads=heads) * len(prompts)
+        def local(sites):  # the reference loop over this rank's (layer, head) sites only
+            out = torch.zeros(cfg.n_layers, cfg.n_heads, dtype=torch.float64)
+            for l in sorted({l for l, _ in sites}):
+                out += R.calculate_average_causal_indirect_effect(
+                    mean, prompts, answers, oracle, layers=[l], heads=[h for ll, h in sites if ll == l])
+            return out * len(prompts)
 
-        cie = D.sharded_cie(cfg.n_layers, cfg.n_heads, len(prompts), local)
+        cie = D.sharded_cie(cfg.n_layers, cfg.n_heads, len(prompts), local,
+                            lambda: torch.zeros(cfg.n_layers, cfg.n_heads, dtype=torch.float64))
         # prompt-sharded extraction with a stand-in "Σ z" and projection
         vecs = torch.randn(10, 3, 4, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
         ids = list(range(10))
         mean_x = D.sharded_mean_activation(ids, lambda ps: vecs[list(ps)].sum(0), lambda z: z * 2,
                                            lambda: torch.zeros(3, 4, dtype=torch.float64))
-        q.put((rank, cie, mean_x, D.strided_shard(cfg.n_heads, rank, world),
+        q.put((rank, cie, mean_x, D.balanced_site_shard(cfg.n_layers, cfg.n_heads, rank, world),
                D.contiguous_shard(10, rank, world)))
     finally:
         dist.destroy_process_group()
@@ -80,14 +84,34 @@ def test_sharded_sweeps_match_single_process(world):
     full = R.calculate_average_causal_indirect_effect(mean, [[0, 5, 1, 9, 44, 1, 7], [0, 3, 1, 8, 1, 12, 19, 1, 6]],
                                                       [[9], [12]], oracle)
     vecs = torch.randn(10, 3, 4, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
-    heads_seen, items_seen = [], []
-    for rank, cie, mean_x, heads, (a, b) in results:
+    sites_seen, items_seen = [], []
+    for rank, cie, mean_x, sites, (a, b) in results:
         torch.testing.assert_close(cie, full, rtol=0, atol=1e-15)
         torch.testing.assert_close(mean_x, vecs.sum(0) * 2 / 10, rtol=1e-14, atol=0)
-        heads_seen += heads
+        sites_seen += sites
         items_seen += list(range(a, b))
-    assert sorted(heads_seen) == list(range(cfg.n_heads))   # every head exactly once
+    assert sorted(sites_seen) == [(l, h) for l in range(cfg.n_layers) for h in range(cfg.n_heads)]  # each once
     assert sorted(items_seen) == list(range(10))            # every prompt exactly once
+
+
+@pytest.mark.parametrize("L,H,world", [(32, 32, 1), (32, 32, 2), (32, 32, 4), (32, 32, 8), (36, 40, 8),
+                                       (36, 40, 2), (12, 12, 3), (5, 4, 2), (2, 4, 4), (3, 2, 4)])
+def test_balanced_site_shard(L, H, world):
+    """Every (layer, head) site on exactly one rank; the staircase work
+    (Σ over a rank's sites of the L - 1 - l blocks after the site) equal on
+    every rank when world divides H; whole layers per rank where the pairs
+    divide evenly (C3: 2.8B on 8 GPUs = 2 layer pairs per rank, every head)."""
+    from tvr_amd import distributed as D
+    shares = [D.balanced_site_shard(L, H, r, world) for r in range(world)]
+    allsites = sorted(s for sh in shares for s in sh)
+    assert allsites == [(l, h) for l in range(L) for h in range(H)]
+    work = [sum(L - 1 - l for l, _ in sh) for sh in shares]
+    if H % world == 0:
+        assert len(set(work)) == 1, work
+    if (L // 2) % world == 0 and L % 2 == 0:
+        for sh in shares:  # whole layers: every head of each of the rank's layers
+            layers = {l for l, _ in sh}
+            assert len(sh) == len(layers) * H
 
 
 # ----------------------------------------------------------- site-sharded sweeps

@@ -4,7 +4,7 @@ on cuda:0 (one GPU per box here; the driver's 8-GPU runs use RCCL).  Each
 rank builds the same seeded tiny model; the sharded results must equal the
 single-process engine results:
 
-* cie_heads_sharded (heads ≡ rank mod 2, one all-reduce)       == calculate_average_causal_indirect_effect
+* cie_sharded (balanced layer-pair sites, one all-reduce)  == calculate_average_causal_indirect_effect
 * mean_activation_sharded (contiguous prompt split, all-reduce) == sum_last_z / n, projected
 * the layer sweeps and the FV layer sweep with (prompt, layer) sites
   round-robin + all_gather                                      == the unsharded sweeps
@@ -50,7 +50,7 @@ def _run(sharded: bool):
     lv = E.gather_head_activations_to_layers(mean)
     fv = mean[0, :2].sum(0)
     if sharded:
-        return {"cie": D.cie_heads_sharded(mean, prompts, answers, model).cpu(),
+        return {"cie": D.cie_sharded(mean, prompts, answers, model).cpu(),
                 "mean": D.mean_activation_sharded(ex, model).cpu(),
                 "acc": D.apply_layered_vectors_to_zero_shot_sharded(lv, task, arrow, model),
                 "dprob": D.apply_layered_vectors_to_zero_shot_by_probability_sharded(lv, task, arrow, model).cpu(),

@@ -87,7 +87,7 @@ def c4(n_tasks, gemm):
         ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, task, arrow, ",", 512, 5)
         mean, t_ex = timed(lambda: D.mean_activation_sharded(ex_prompts, model))
         prompts, answers = E.generate_shuffled_prompts(task, model, 12, 5, arrow)
-        cie, t_cie = timed(lambda: D.cie_heads_sharded(mean, prompts, answers, model))
+        cie, t_cie = timed(lambda: D.cie_sharded(mean, prompts, answers, model))
         fv = E.assemble_task_vector(mean, cie, 10, 10)
         acc, t_fv = timed(lambda: D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, task, 5, model))
         per_task.append({"task_seed": 100 + ti, "extraction_s": round(t_ex, 3), "cie_s": round(t_cie, 3),
