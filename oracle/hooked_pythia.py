@@ -141,9 +141,12 @@ class HookedPythiaOracle:
     """Batch-1-oriented CPU model with TL hook semantics (works for any batch)."""
 
     def __init__(self, cfg: OracleConfig, hf_state_dict: Dict[str, torch.Tensor],
-                 dtype=torch.float32, tokenizer=None):
+                 dtype=torch.float32, tokenizer=None, rotary_table_dtype=None):
         self.cfg = cfg
         self.dtype = dtype
+        # TL computes sin / cos in fp32, or fp64 for an fp64 model; ``rotary_table_dtype=torch.float32``
+        # evaluates the fp32 reference's tables in this (e.g. fp64) model (oracle/streamed_pythia.py)
+        self._table_dtype = rotary_table_dtype
         # processed where the state dict lives (a GPU-resident one processes in
         # seconds), then kept on the CPU: the oracle always runs on the CPU
         self.w = _cpu(tl_process_weights(hf_state_dict, cfg, dtype))
@@ -154,7 +157,7 @@ class HookedPythiaOracle:
 
     # --- TL calculate_sin_cos_rotary (non-adjacent pairs: repeat "(2 d)") ---
     def _rotary_tables(self, rd: int, n_ctx: int, base: float):
-        hp = torch.float64 if self.dtype == torch.float64 else torch.float32
+        hp = self._table_dtype or (torch.float64 if self.dtype == torch.float64 else torch.float32)
         pos = torch.arange(n_ctx, dtype=hp)
         dim = torch.arange(rd // 2, dtype=hp)
         freq = base ** (dim / (rd / 2))

@@ -1,0 +1,126 @@
+"""ORACLE (test infrastructure only) — the layer-streamed fp64 oracle with
+selected intermediates ROUNDED to a narrower type, the way a GEMM path rounds
+them: fp32 (what the reference's own fp32 arithmetic does), bf16 / fp16 (the
+engine's 16-bit GEMM operands: weights, LayerNorm outputs, z, GELU(h), the
+final norm's output).  It measures how much error a rounding scheme alone
+produces at full depth — the floor any implementation of that arithmetic
+has — so the bf16 parity test can hold the engine to "no more than its own
+operand roundings explain" (tests/test_gpu_full_depth.py), and
+tools/precision_probe.py can rank the rounding points.  Everything not
+rounded stays fp64; the rounding points follow csrc/ (split.hpp store_ln4: the
+bf16 mode's Q / K operands are fp16, the rest bf16).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .streamed_pythia import StreamedPythiaOracle
+
+
+def r16(x, dtype):
+    """Round to a 16-bit type; fp16 with a power-of-two scale into its range (as the engine's planes)."""
+    if dtype == torch.bfloat16:
+        return x.to(torch.bfloat16).to(x.dtype)
+    m = x.abs().max().item()
+    s = 2.0 ** (14 - math.ceil(math.log2(m))) if m > 0 else 1.0
+    return (x * s).to(torch.float16).to(x.dtype) / s
+
+
+class Rounded(StreamedPythiaOracle):
+    """fp64 streamed oracle with rounding points.  ``rules``: name -> callable(x)."""
+
+    def __init__(self, cfg, get_raw, rules):
+        self.rules = rules
+        super().__init__(cfg, get_raw)
+        self._wcache = {}
+
+    def R(self, name, x):
+        f = self.rules.get(name)
+        return f(x) if f else x
+
+    def block(self, l):
+        b = super().block(l)
+        if self._wcache.get("l") != l:
+            self._wcache = {"l": l, "w": {k: self.R("w_" + k, v) for k, v in b.items()}}
+        return self._wcache["w"]
+
+    def _ln_pre(self, x):
+        x = self.R("ln_in", x)
+        y = super()._ln_pre(x)
+        return self.R("ln_out", y)
+
+    def _block(self, l, resid, replace=(), add_last=(), want_result_last=False):
+        w = self.block(l)
+        x = self._ln_pre(resid)
+        xq = self.R("a_qk", x)
+        xv = self.R("a_v", x)
+        q = self._rotate(self.R("gemm_out", torch.einsum("bpd,hde->bphe", xq, w["W_Q"]) + w["b_Q"]))
+        k = self._rotate(self.R("gemm_out", torch.einsum("bpd,hde->bphe", xq, w["W_K"]) + w["b_K"]))
+        v = self.R("gemm_out", torch.einsum("bpd,hde->bphe", xv, w["W_V"]) + w["b_V"])
+        T = x.shape[1]
+        scores = self.R("attn", torch.einsum("bqhe,bkhe->bhqk", q, k) / math.sqrt(self.cfg.d_head))
+        mask = torch.triu(torch.ones(T, T, dtype=torch.bool, device=x.device), diagonal=1)
+        pat = self.R("attn", torch.softmax(scores.masked_fill(mask, float("-inf")), dim=-1))
+        z = self.R("attn", torch.einsum("bkhe,bhqk->bqhe", v, pat))
+        H, dh, d = self.cfg.n_heads, self.cfg.d_head, self.cfg.d_model
+        zo = self.R("a_z", z)
+        attn = self.R("gemm_out", zo.reshape(z.shape[0], T, H * dh) @ w["W_O"].reshape(H * dh, d))
+        if replace:
+            rows = sorted({r for r, _, _ in replace})
+            ri = torch.tensor(rows, device=x.device)
+            result = torch.einsum("bqhe,hed->bqhd", zo[ri], w["W_O"])
+            at = {r: i for i, r in enumerate(rows)}
+            for r, h, vec in replace:
+                result[at[r], :, h, :] = vec.to(result)
+            attn[ri] = result.sum(-2)
+        for r, vec in add_last:
+            attn[r, -1] = attn[r, -1] + vec.to(attn)
+        h = self.R("gemm_out", xv @ w["W_in"] + w["b_in"])
+        g = self.R("a_gelu", torch.nn.functional.gelu(h))
+        mlp = self.R("gemm_out", g @ w["W_out"])
+        res_last = torch.einsum("bhe,hed->bhd", z[:, -1], w["W_O"]) if want_result_last else None
+        return self.R("resid", resid + (attn + w["b_O"]) + (mlp + w["b_out"])), res_last
+
+    def _final_last(self, resid):
+        x = self.R("a_u", self._ln_pre(resid[:, -1]))
+        return x @ self.R("w_U", self.W_U) + self.b_U
+
+
+def x2f16(x):
+    """The engine's fp32-accurate split (csrc/split.hpp): s x = fp16(s x) + fp16(s x - fp16(s x)), s a power of
+    two putting max |x| in fp16's range; the value the three-product GEMM sees (22 significand bits)."""
+    m = x.abs().max().item()
+    s = 2.0 ** (14 - math.ceil(math.log2(m))) if m > 0 else 1.0
+    y = (x * s).float()
+    h0 = y.half().float()
+    h1 = (y - h0).half().float()
+    return (h0.double() + h1.double()) / s
+
+
+F32 = lambda x: x.float().double()  # noqa: E731
+BF = lambda x: r16(x, torch.bfloat16)  # noqa: E731
+FH = lambda x: r16(x, torch.float16)  # noqa: E731
+WEIGHTS = ["w_W_Q", "w_W_K", "w_W_V", "w_W_O", "w_W_in", "w_W_out", "w_U"]
+ACTS = ["a_qk", "a_v", "a_z", "a_gelu", "a_u"]
+
+
+def variants():
+    v = {"fp64": {},
+         "fp32_all": {k: F32 for k in ["ln_in", "ln_out", "gemm_out", "attn", "resid", "a_gelu"] + WEIGHTS},
+         "resid32": {"resid": F32}, "ln32": {"ln_in": F32, "ln_out": F32}, "attn32": {"attn": F32},
+         "gemm32": {"gemm_out": F32}, "gelu32": {"a_gelu": F32}, "w32": {k: F32 for k in WEIGHTS}}
+    allbf = {k: BF for k in WEIGHTS + ACTS}
+    v["all_bf16"] = allbf
+    eng = dict(allbf, a_qk=FH, w_W_Q=FH, w_W_K=FH)
+    v["engine_bf16"] = eng
+    v["w_bf16"] = {k: BF for k in WEIGHTS}
+    v["act_bf16"] = {k: BF for k in ACTS}
+    v["all_f16"] = {k: FH for k in WEIGHTS + ACTS}
+    # the x2f16 GEMM path: every GEMM operand split into two fp16 planes, the rest of the arithmetic fp32
+    v["x2f16_ops"] = {k: x2f16 for k in WEIGHTS + ACTS}
+    v["x2f16_engine"] = dict(v["fp32_all"], **{k: x2f16 for k in WEIGHTS + ACTS})
+    for k in WEIGHTS + ACTS:  # the engine's bf16 mode with ONE operand group kept exact
+        v["engine_bf16_but_" + k] = {kk: vv for kk, vv in eng.items() if kk != k}
+    return v

@@ -50,7 +50,8 @@ from .hooked_pythia import OracleConfig, tl_process_block, tl_process_embed, tl_
 
 
 class StreamedPythiaOracle:
-    def __init__(self, cfg: OracleConfig, get_raw: Callable[[str], torch.Tensor], dtype=torch.float64):
+    def __init__(self, cfg: OracleConfig, get_raw: Callable[[str], torch.Tensor], dtype=torch.float64,
+                 rotary_table_dtype=torch.float32):
         self.cfg = cfg
         self.dtype = dtype
         self._get = get_raw
@@ -59,9 +60,14 @@ class StreamedPythiaOracle:
         self.device = self.W_E.device
         self.W_U, self.b_U = tl_process_unembed(g("embed_out.weight"), g("gpt_neox.final_layer_norm.weight"),
                                                 g("gpt_neox.final_layer_norm.bias"))
-        # TL calculate_sin_cos_rotary: fp32 tables, fp64 for an fp64 model (as HookedPythiaOracle)
+        # TL calculate_sin_cos_rotary computes the tables in fp32 for any model dtype but fp64: the reference
+        # runs fp32 (TL's default), so its tables are the fp32 ones, which this fp64 evaluation keeps
+        # (``rotary_table_dtype``; float64 restates an fp64 TL model instead).  At 12B (T = 33) the fp32
+        # angles pos / freq differ from fp64 by up to ~2e-6 rad — 30x the fp32 rounding of q / k, and the
+        # largest single difference between the fp32 reference and an fp64-table model
+        # (tools/precision_probe.py): a model definition, not arithmetic error.
         rd = cfg.rotary_dim
-        hp = torch.float64 if dtype == torch.float64 else torch.float32
+        hp = rotary_table_dtype
         pos = torch.arange(cfg.n_ctx, dtype=hp, device=self.device)
         dim = torch.arange(max(rd // 2, 1), dtype=hp, device=self.device)
         freq = cfg.rotary_base ** (dim / max(rd / 2, 1))

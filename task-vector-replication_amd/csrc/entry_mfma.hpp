@@ -10,11 +10,15 @@
 // Grid = (groups, ceil(d / 256)), 4 waves of 64 columns each; a group is up to
 // ENTRY_GROUP sites of one head (the host groups a layer's REPLACE_HEAD entries),
 // whose W_O[h] columns the wave reads once into registers: the launch was bound
-// by re-reading the 80 KB W_O slice of a 256-column block for every site.  The
+// by re-reading the 80 KB W_O slice of a 256-column block for every site (at
+// C3 a layer's 12 prompts x 32 heads: 12 sites per head, one group).  The
 // MFMA's k index is a permutation applied to both operands: lane group g
-// supplies k = g CH + j at k-step j (CH = dh / 4), so a lane's B
-// operand is CH consecutive floats of one W_O row (float4 loads) and its A
-// operand CH consecutive floats of one z row, read from the z tile in LDS.
+// supplies k = g CH + j at k-step j (CH = dh / 4), so a lane's A operand is CH
+// consecutive floats of one W_O row (float4 loads) and its B operand CH
+// consecutive floats of one z row, read from the z tile in LDS.  With W_O as
+// the A operand the product is D[column][position]: each lane ends with four
+// consecutive columns of one position, so the clean rows, the vector and the
+// patched rows move as 16-B accesses (64 B of a row per lane group).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -24,7 +28,7 @@
 
 namespace tvr {
 
-constexpr int ENTRY_GROUP = 4;  // sites of one head per block: W_O[h] read once for them
+constexpr int ENTRY_GROUP = 16;  // sites of one head per block: W_O[h] read once for them
 
 template <int DH>
 __global__ void __launch_bounds__(ENTRY_THREADS)
@@ -67,18 +71,17 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
       }
       __syncthreads();
       if (n0 >= d) continue;  // (a wave past d joins the barriers only)
-      // the clean rows' values and the vector first (no load between the stores below)
-      f32x4 sv[4];
-      float vc[4];
+      // the clean rows' values and the vector first (no load between the stores below); lane (li, g) owns
+      // position li and columns n0 + 16 nt + 4 g .. + 3
+      const int pr = min(li, tn - 1);
+      f32x4 sv[4], vc[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const int c = min(n0 + 16 * nt + li, d - 1);
-        vc[nt] = vectors[(size_t)e.vec * d + c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sv[nt][r] = snap[(size_t)(e.src_row + e.p0 + t0 + min(4 * g + r, tn - 1)) * d + c];
+        const int c = min(n0 + 16 * nt + 4 * g, d - 4);
+        vc[nt] = *(const f32x4*)(vectors + (size_t)e.vec * d + c);
+        sv[nt] = *(const f32x4*)(snap + (size_t)(e.src_row + e.p0 + t0 + pr) * d + c);
       }
-      float za[CH];  // A operand: z row li, k = g CH ..
+      float za[CH];  // B operand: z row li, k = g CH ..
 #pragma unroll
       for (int q = 0; q < CH; q += 4) {
         const f32x4 v4 = *(const f32x4*)(zt + li * LDZ + g * CH + q);
@@ -90,18 +93,17 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};  // two chains (dependent-issue latency)
 #pragma unroll
         for (int j = 0; j < CH; j += 2) {
-          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j], wb[nt][j], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j + 1], wb[nt][j + 1], a1, 0, 0, 0);
+          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[nt][j], za[j], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wb[nt][j + 1], za[j + 1], a1, 0, 0, 0);
         }
-        acc[nt] = a0 + a1;  // D[position 4 g + r][column li]
+        acc[nt] = a0 + a1;  // D[column 16 nt + 4 g + r][position li]
       }
+      if (li < tn) {
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int c = n0 + 16 * nt + li;
-        if (c >= d) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * g + r < tn) resid[(size_t)(e.row0 + t0 + 4 * g + r) * d + c] = sv[nt][r] + (vc[nt] - acc[nt][r]);
+        for (int nt = 0; nt < 4; ++nt) {
+          const int c = n0 + 16 * nt + 4 * g;
+          if (c < d) *(f32x4*)(resid + (size_t)(e.row0 + t0 + li) * d + c) = sv[nt] + (vc[nt] - acc[nt]);
+        }
       }
     }
   }

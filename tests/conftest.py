@@ -51,8 +51,12 @@ def tokenizer(tiny_cfg):
     return tvr_amd.tokenizer.SyntheticTokenizer(tiny_cfg.d_vocab)
 
 
-def make_oracle(cfg, sd, tokenizer, dtype=torch.float32):
-    return HookedPythiaOracle(oracle_config(cfg), sd, dtype=dtype, tokenizer=tokenizer)
+def make_oracle(cfg, sd, tokenizer, dtype=torch.float32, rotary_table_dtype=None):
+    """``rotary_table_dtype=torch.float32`` with an fp64 ``dtype``: the fp32
+    reference evaluated in fp64 (TL computes an fp32 model's sin / cos tables
+    in fp32: oracle/streamed_pythia.py)."""
+    return HookedPythiaOracle(oracle_config(cfg), sd, dtype=dtype, tokenizer=tokenizer,
+                              rotary_table_dtype=rotary_table_dtype)
 
 
 @pytest.fixture(scope="session")

@@ -21,17 +21,21 @@ tests/test_streamed_oracle.py.  No bar depends on the engine under test.
   layers, 10-shot T = 33; x2f16, the C5 path; the fp32 MFMA path is reported)
   at layers {0, 18, 35} x all 40 heads.  Max |CIE| > 1e-3 is asserted (the
   sites move the probability).
-* C4, Pythia-6.9B in the bf16 configuration (``test_c4_bf16_function_vector_
-  pipeline``): extraction over 64 five-shot prompts (max-abs relative < 2e-2,
-  the north star's bf16 bar); the CIE of 12 prompts over layers 0 .. 10, 16,
-  31 x all heads with the oracle's means (error reported as a fraction of
-  max |CIE|); the top-10 function-vector head set of layers <= 10
-  (scratch2.py:232-238, C4's FV) identical to the oracle's; then the whole C4
-  chain on the engine's own means and CIE — FV assembled, added at layer 10
-  of 50 zero-shot prompts, top-5 accuracy (scratch2.py:292-304) identical to
-  the oracle chain's, clean and with the FV.
+* C4, Pythia-6.9B (``test_c4_function_vector_pipeline``): extraction over 64
+  five-shot prompts; the CIE of 12 prompts over layers 0 .. 10, 16, 31 x all
+  heads with the oracle's means; the top-10 function-vector head set of layers
+  <= 10 (scratch2.py:232-238, C4's FV); then the whole C4 chain on the
+  engine's own means and CIE — FV assembled, added at layer 10 of 50 zero-shot
+  prompts, top-5 accuracy (scratch2.py:292-304), clean and with the FV.  On
+  the fp32-accurate x2f16 path every one of these is held to the fp32 bars
+  (head set and accuracies identical); on bf16, the north star's 2e-2 on the
+  extracted vectors and a CIE error no larger than 1.5x the error bf16
+  rounding of the same GEMM operands produces in the fp64 oracle
+  (oracle/rounded_pythia.py) — see the test's docstring for why the head set
+  cannot be a bf16 requirement.
 The CIE answers are the clean argmax (random pairs give p ~ 1e-5 and a
-vacuous CIE); the zero-shot task's answers are the oracle's own clean top-1.
+vacuous CIE); the zero-shot task's answers are the oracle's clean second
+choice (top-5 accuracy 1 without the FV; the FV moves them).
 """
 import random
 
@@ -133,74 +137,103 @@ def test_full_depth_fp32_paths(which):
 
 
 FV_LAYER, FV_HEADS = 10, 10  # C4: the function vector of the top-10 heads with layer <= 10 (scratch2.py:270 scaled)
+_C4 = {}
 
 
-@pytest.mark.timeout(900)
-def test_c4_bf16_function_vector_pipeline():
+def c4_reference():
+    """Pythia-6.9B (32 layers, std-0.05 weights) and the oracle's side of the
+    C4 chain, computed once: extraction over 64 five-shot prompts, the CIE of
+    12 prompts over layers 0..10, 16, 31, the top-10 FV heads of layers <= 10,
+    the FV's top-5 accuracy on 50 zero-shot prompts."""
+    if _C4:
+        return _C4
     name = "pythia-6.9b"
     cfg = tvr_amd.get_config(name)
     b = _Builder(cfg)
-    model = tvr_amd.Model.from_pretrained(name, device="cuda", seed=0, std=STD, gemm="bf16")
     oracle = streamed_oracle(cfg)
-    L, H = cfg.n_layers, cfg.n_heads
+    H = cfg.n_heads
+    task = tvr_amd.tasks.synthetic_task(50, cfg.d_vocab, seed=101)
+    random.seed(5)
+    ex = tvr_amd.prompts.sample_icl_prompts(b, task, ARROW, ",", 64, 5)
+    mean_ref = oracle.mean_activation(ex)
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(b, 12, 5, seed=1234)
+    answers = [int(r.argmax()) for r in oracle.last_logits(prompts)]
+    layers = list(range(FV_LAYER + 1)) + [16, 31]
+    mean32 = mean_ref.float()  # the vectors both sides patch with
+    cie_ref = oracle.cie(mean32.double(), prompts, answers, layers=layers)
+    top = torch.topk(cie_ref[:FV_LAYER + 1].flatten(), FV_HEADS + 1)
+    fv_ref = E.assemble_task_vector(mean_ref, cie_ref, FV_LAYER, FV_HEADS)
+    # zero-shot task: the answers are the oracle's clean SECOND choice after [BOS, x, ":"] (clean top-5 accuracy 1;
+    # the FV moves them in and out of the top 5)
+    xs = [f"<|{t}|>" for t in random.Random(9).sample(range(1000, cfg.d_vocab), 50)]
+    zs = [[0, b.tokenizer.encode(x)[0], b.tokenizer.encode(":")[0]] for x in xs]
+    base_top = oracle.added_topk(zs, FV_LAYER, None, 5)
+    dec = b.tokenizer.decode_one
+    contexts = [(x, dec(int(t[1]))) for x, t in zip(xs, base_top)]
+    firsts = [dec(b.tokenizer.encode(y)[0]) for _, y in contexts]  # scratch2.py:298: decoded strings
+
+    def acc(tops):
+        return sum(f in [dec(int(t)) for t in row] for f, row in zip(firsts, tops)) / len(zs)
+    _C4.update(cfg=cfg, name=name, oracle=oracle, ex=ex, mean_ref=mean_ref, mean32=mean32, prompts=prompts,
+               answers=answers, layers=layers, cie_ref=cie_ref, cmax=cie_ref.abs().max().item(),
+               set_ref=sorted(divmod(int(i), H) for i in top.indices[:FV_HEADS]),
+               gap=(top.values[FV_HEADS - 1] - top.values[FV_HEADS]).item(), contexts=contexts,
+               acc_ref=(acc(base_top), acc(oracle.added_topk(zs, FV_LAYER, fv_ref, 5))))
+    return _C4
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("gemm", ["x2f16", "bf16"])
+def test_c4_function_vector_pipeline(gemm):
+    """C4 at full depth.  x2f16 (fp32-accurate): the north star's fp32 bars —
+    extraction 1e-4, CIE 1e-4 max|CIE| + 1e-7, the top-10 FV head set and the
+    FV top-5 accuracy identical, in isolation (the oracle's means) and along
+    the engine's own chain.  bf16: the north star's bf16 bar on the extracted
+    vectors (2e-2); its CIE error must not exceed 1.5x what bf16 rounding of
+    the GEMM operands alone produces (oracle/rounded_pythia.py: the fp64
+    oracle with the engine's operand roundings, measured on the same sites):
+    the 10th and 11th oracle CIE values are ~1e-3 of max |CIE| apart, two
+    orders of magnitude inside bf16's ~1e-1 CIE noise, so the top-10 set is a
+    fp32-accurate requirement (asserted on x2f16) and reported for bf16."""
+    r = c4_reference()
+    cfg, H = r["cfg"], r["cfg"].n_heads
+    model = tvr_amd.Model.from_pretrained(r["name"], device="cuda", seed=0, std=STD, gemm=gemm)
     try:
-        # --- a1: extraction over 64 five-shot prompts of a synthetic 50-pair task (C4's prompt form)
-        task = tvr_amd.tasks.synthetic_task(50, cfg.d_vocab, seed=101)
-        random.seed(5)
-        ex = tvr_amd.prompts.sample_icl_prompts(b, task, ARROW, ",", 64, 5)
-        mean_ref = oracle.mean_activation(ex)
+        ex, prompts, answers, layers, cmax = r["ex"], r["prompts"], r["answers"], r["layers"], r["cmax"]
         mean_eng = model.project_heads(E.sum_last_z(model, ex)) / len(ex)
-        e_mean = rel_err(mean_eng, mean_ref)
-        print(f"C4 bf16 extraction: max-abs rel {e_mean:.3e} (max |mean| {mean_ref.abs().max():.3e})")
-        # --- a7: CIE over 12 prompts (T = 18), layers 0..10, 16, 31 x all heads, with the oracle's means
-        prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(b, 12, 5, seed=1234)
-        clean_ref = oracle.last_logits(prompts)
-        answers = [int(r.argmax()) for r in clean_ref]
-        p_max = torch.softmax(clean_ref, -1).max().item()
-        layers = list(range(FV_LAYER + 1)) + [16, 31]
-        mean32 = mean_ref.float()
-        cie_ref = oracle.cie(mean32.double(), prompts, answers, layers=layers)
-        cie = (E.causal_indirect_effect_sums(mean32.cuda(), prompts, answers, model, layers=layers).cpu().double()
-               / len(prompts))
-        cmax = cie_ref.abs().max().item()
-        err = (cie - cie_ref).abs()
-        rep = {l: err[l].max().item() / cmax for l in (0, 16, 31)}
-        print(f"C4 bf16 CIE: max |CIE| {cmax:.3e}, p_max {p_max:.3f}; |err| / max|CIE| at layers 0/16/31 "
-              f"{rep[0]:.2e} / {rep[16]:.2e} / {rep[31]:.2e}, over layers <= {FV_LAYER} "
-              f"{err[:FV_LAYER + 1].max().item() / cmax:.2e}")
-        top_ref = torch.topk(cie_ref[:FV_LAYER + 1].flatten(), FV_HEADS + 1)
-        top_eng = torch.topk(cie[:FV_LAYER + 1].flatten(), FV_HEADS)
-        set_ref = sorted(divmod(int(i), H) for i in top_ref.indices[:FV_HEADS])
-        set_eng = sorted(divmod(int(i), H) for i in top_eng.indices)
-        gap = (top_ref.values[FV_HEADS - 1] - top_ref.values[FV_HEADS]).item()
-        print(f"C4 bf16 top-{FV_HEADS} heads (layer <= {FV_LAYER}): oracle {set_ref}, engine {set_eng}; oracle gap "
-              f"10th-11th {gap:.2e}, engine max |err| there {err[:FV_LAYER + 1].max().item():.2e}")
-        # --- the whole C4 chain on the engine's own means and CIE vs the oracle's chain
+        e_mean = rel_err(mean_eng, r["mean_ref"])
+        cie = (E.causal_indirect_effect_sums(r["mean32"].cuda(), prompts, answers, model, layers=layers)
+               .cpu().double() / len(prompts))
+        err = (cie - r["cie_ref"]).abs()
+        set_eng = sorted(divmod(int(i), H) for i in torch.topk(cie[:FV_LAYER + 1].flatten(), FV_HEADS).indices)
+        # the chain on the engine's own means and CIE (bench C4's computation)
         cie_chain = (E.causal_indirect_effect_sums(mean_eng, prompts, answers, model,
                                                    layers=list(range(FV_LAYER + 1))).cpu().double() / len(prompts))
-        fv_ref = E.assemble_task_vector(mean_ref, cie_ref, FV_LAYER, FV_HEADS)
-        fv_eng = E.assemble_task_vector(mean_eng, cie_chain.to(mean_eng.device), FV_LAYER, FV_HEADS)
         set_chain = sorted(divmod(int(i), H) for i in torch.topk(cie_chain[:FV_LAYER + 1].flatten(), FV_HEADS).indices)
-        print(f"C4 bf16 chain: top-{FV_HEADS} heads {set_chain}, FV rel err {rel_err(fv_eng, fv_ref):.3e}")
-        # zero-shot task: 50 items whose answers are the oracle's clean top-1 of [BOS, x, ":"]
-        xs = [f"<|{t}|>" for t in random.Random(9).sample(range(1000, cfg.d_vocab), 50)]
-        zs = [[0, b.tokenizer.encode(x)[0], b.tokenizer.encode(":")[0]] for x in xs]
-        base_top = oracle.added_topk(zs, FV_LAYER, None, 5)
-        contexts = [(x, b.tokenizer.decode_one(int(t[0]))) for x, t in zip(xs, base_top)]
-        fv_top = oracle.added_topk(zs, FV_LAYER, fv_ref, 5)
-        dec = b.tokenizer.decode_one
-        firsts = [dec(b.tokenizer.encode(y)[0]) for _, y in contexts]  # scratch2.py:298: decoded strings
-
-        def acc(tops):
-            return sum(f in [dec(int(t)) for t in row] for f, row in zip(firsts, tops)) / len(zs)
-        acc_ref = (acc(base_top), acc(fv_top))
-        acc_eng = E.check_accuracy_of_task_vector(fv_eng, FV_LAYER, contexts, 5, model=model)
-        print(f"C4 bf16 FV top-5 accuracy at layer {FV_LAYER} (clean, with FV): engine {acc_eng}, oracle {acc_ref}")
-        assert e_mean < 2e-2, e_mean
+        fv_eng = E.assemble_task_vector(mean_eng, cie_chain.to(mean_eng.device), FV_LAYER, FV_HEADS)
+        acc_eng = tuple(E.check_accuracy_of_task_vector(fv_eng, FV_LAYER, r["contexts"], 5, model=model))
+        overlap = len(set(set_eng) & set(r["set_ref"]))
+        print(f"C4 {gemm}: extraction max-abs rel {e_mean:.3e}; CIE max |CIE| {cmax:.3e}, |err| / max|CIE| at "
+              f"layers 0/16/31 {err[0].max() / cmax:.2e} / {err[16].max() / cmax:.2e} / {err[31].max() / cmax:.2e}, "
+              f"all {err.max() / cmax:.2e}; top-{FV_HEADS} heads (layer <= {FV_LAYER}) oracle {r['set_ref']}, engine "
+              f"{set_eng} ({overlap} shared; oracle 10th-11th gap {r['gap']:.2e}), chain {set_chain}; FV top-5 "
+              f"accuracy (clean, FV) engine {acc_eng} oracle {r['acc_ref']}")
         assert cmax > 1e-3
-        assert set_eng == set_ref, (set_eng, set_ref)
-        assert set_chain == set_ref, (set_chain, set_ref)
-        assert tuple(acc_eng) == tuple(acc_ref), (acc_eng, acc_ref)
+        if gemm == "x2f16":
+            assert e_mean < TOL, e_mean
+            assert err.max().item() <= TOL * cmax + 1e-7, (err.max().item(), cmax)
+            assert set_eng == r["set_ref"], (set_eng, r["set_ref"])
+            assert set_chain == r["set_ref"], (set_chain, r["set_ref"])
+            assert acc_eng == r["acc_ref"], (acc_eng, r["acc_ref"])
+        else:
+            from oracle.rounded_pythia import Rounded, variants
+            shapes = tvr_amd.weights.hf_param_shapes(cfg)
+            emu = Rounded(oracle_config(cfg), lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", STD),
+                          variants()["engine_bf16"])
+            floor = (emu.cie(r["mean32"].double(), prompts, answers, layers=layers) - r["cie_ref"]).abs().max().item()
+            print(f"C4 bf16: emulated bf16-operand floor {floor / cmax:.2e} of max |CIE|, engine {err.max() / cmax:.2e}")
+            assert e_mean < 2e-2, e_mean
+            assert err.max().item() <= 1.5 * floor, (err.max().item(), floor)
     finally:
         del model
         torch.cuda.empty_cache()

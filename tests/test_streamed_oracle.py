@@ -9,8 +9,9 @@ import pytest
 import torch
 
 import tvr_amd
-from conftest import TINY_STD, make_oracle
+from conftest import TINY_STD
 from oracle import reference_experiments as R
+from oracle.hooked_pythia import HookedPythiaOracle
 from oracle.streamed_pythia import StreamedPythiaOracle
 
 from conftest import oracle_config
@@ -29,8 +30,10 @@ def pair():
     def get_raw(name):
         calls.append(name)
         return sd[name].clone()
-    streamed = StreamedPythiaOracle(oracle_config(cfg), get_raw)
-    return cfg, tok, make_oracle(cfg, sd, tok, torch.float64), streamed, calls
+    streamed = StreamedPythiaOracle(oracle_config(cfg), get_raw)  # the fp32 reference's rotary tables
+    full = HookedPythiaOracle(oracle_config(cfg), sd, dtype=torch.float64, tokenizer=tok,
+                              rotary_table_dtype=torch.float32)
+    return cfg, tok, full, streamed, calls
 
 
 def rel(a, b):
@@ -101,3 +104,17 @@ def test_added_vector_topk_equals_reference_hook(pair):
     clean = streamed.added_topk(seqs, 0, None, 3)
     for s, row in zip(seqs, clean):
         assert row.tolist() == torch.topk(full.forward(torch.tensor([s]))[0, -1], 3).indices.tolist()
+
+
+def test_rotary_tables_are_the_fp32_references():
+    """The fp64 evaluation keeps the fp32 reference's sin / cos tables (TL
+    computes them in fp32 for an fp32 model): identical to HookedPythiaOracle's
+    fp32 tables; fp64 tables are a different (fp64 TL) model."""
+    cfg = tvr_amd.get_config("tiny")
+    shapes = tvr_amd.weights.hf_param_shapes(cfg)
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, "cpu") for n, s in shapes.items()}
+    st = StreamedPythiaOracle(oracle_config(cfg), lambda n: sd[n])
+    h32 = HookedPythiaOracle(oracle_config(cfg), sd)
+    h64 = HookedPythiaOracle(oracle_config(cfg), sd, dtype=torch.float64)
+    assert torch.equal(st._sin, h32._sin.double()) and torch.equal(st._cos, h32._cos.double())
+    assert not torch.equal(st._sin, h64._sin)
