@@ -99,6 +99,34 @@ def x2f16(x):
     return (h0.double() + h1.double()) / s
 
 
+def _ftz16(h):
+    """fp16 values below the smallest normal (2^-14) flushed to zero."""
+    return torch.where(h.abs() < 2.0 ** -14, torch.zeros_like(h), h)
+
+
+def x2f16_act(x, scale=16.0, ftz=False):
+    """The engine's activation split (csrc/split.hpp): a fixed scale (X2_ASCALE = 16), fp16(16 a) +
+    fp16(16 a - fp16(16 a)); ``ftz``: fp16 subnormals read as zero (as a matrix core that flushes them)."""
+    y = (x * scale).float()
+    h0 = y.half().float()
+    h1 = (y - h0).half().float()
+    if ftz:
+        h0, h1 = _ftz16(h0), _ftz16(h1)
+    return (h0.double() + h1.double()) / scale
+
+
+def x2f16_weight(x, ftz=False):
+    """The weight planes: one power-of-two scale per matrix putting max |W| in [2^14, 2^15]."""
+    m = x.abs().max().item()
+    s = 2.0 ** (14 - math.floor(math.log2(m))) if m > 0 else 1.0
+    y = (x * s).float()
+    h0 = y.half().float()
+    h1 = (y - h0).half().float()
+    if ftz:
+        h0, h1 = _ftz16(h0), _ftz16(h1)
+    return (h0.double() + h1.double()) / s
+
+
 F32 = lambda x: x.float().double()  # noqa: E731
 BF = lambda x: r16(x, torch.bfloat16)  # noqa: E731
 FH = lambda x: r16(x, torch.float16)  # noqa: E731
@@ -121,6 +149,15 @@ def variants():
     # the x2f16 GEMM path: every GEMM operand split into two fp16 planes, the rest of the arithmetic fp32
     v["x2f16_ops"] = {k: x2f16 for k in WEIGHTS + ACTS}
     v["x2f16_engine"] = dict(v["fp32_all"], **{k: x2f16 for k in WEIGHTS + ACTS})
+    # the engine's split exactly: activations at the fixed scale 16, weights per matrix; with and without
+    # fp16 subnormals; and a larger activation scale
+    for tag, fa, fw in (("x2e", lambda x: x2f16_act(x), x2f16_weight),
+                        ("x2e_ftz", lambda x: x2f16_act(x, ftz=True), lambda x: x2f16_weight(x, ftz=True)),
+                        ("x2e_a256", lambda x: x2f16_act(x, 256.0), x2f16_weight),
+                        ("x2e_a256_ftz", lambda x: x2f16_act(x, 256.0, True), lambda x: x2f16_weight(x, ftz=True))):
+        v[tag] = dict(v["fp32_all"], **{k: fw for k in WEIGHTS}, **{k: fa for k in ACTS})
+        v[tag + "_acts_only"] = {k: fa for k in ACTS}
+        v[tag + "_gelu_only"] = {"a_gelu": fa}
     for k in WEIGHTS + ACTS:  # the engine's bf16 mode with ONE operand group kept exact
         v["engine_bf16_but_" + k] = {kk: vv for kk, vv in eng.items() if kk != k}
     return v

@@ -1385,8 +1385,9 @@ int tvr_model_range_status(tvr_model* m, void* stream) {
   if (h == 0) return TVR_OK;
   TVR_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(unsigned), st));
   TVR_HIP(hipStreamSynchronize(st));
-  return fail(TVR_ERR_RANGE, "a GEMM input reached |a| >= 4095, outside the fp16-split (X2F16) range; "
-                             "results since the last check are not fp32-accurate: use gemm mode x3bf16 or f32");
+  return fail(TVR_ERR_RANGE, "a GEMM input reached |a| >= " + std::to_string((int)(X2_FP16_OVERFLOW / X2_ASCALE)) +
+                                 ", outside the fp16-split (X2F16) range; results since the last check are not "
+                                 "fp32-accurate: use gemm mode x3bf16 or f32");
 }
 
 int tvr_profile_enable(tvr_model* m, int32_t on) {

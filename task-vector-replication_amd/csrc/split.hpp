@@ -49,7 +49,10 @@ __device__ __forceinline__ void wave_argmax(float& bv, int& bi) {
 // projections (Q, K columns of W1), see engine.hip launch_w1.
 enum ActFmt { ACT_F32 = 0, ACT_X2F16 = 1, ACT_BF16 = 2, ACT_F16 = 3 };
 
-constexpr float X2_ASCALE = 16.0f;
+#ifndef TVR_X2_ASCALE
+#define TVR_X2_ASCALE 16.0f
+#endif
+constexpr float X2_ASCALE = TVR_X2_ASCALE;
 constexpr float X2_FP16_OVERFLOW = 65520.0f;  // fp16(x) is inf from here (round to nearest)
 
 struct SplitF16 {
