@@ -66,6 +66,26 @@ class Rounded(StreamedPythiaOracle):
         z = self.R("attn", torch.einsum("bkhe,bhqk->bqhe", v, pat))
         H, dh, d = self.cfg.n_heads, self.cfg.d_head, self.cfg.d_model
         zo = self.R("a_z", z)
+        acc = self.rules.get("acc")  # (splits of the O + MLP-out GEMM, splits of the others) or None
+        if acc and not replace and not add_last:
+            # the engine's fused GEMMs with fp32 accumulation: [Q|K|V|MLP-in] = xn W1^T, [O|MLP-out] over
+            # K = d + d_mlp in one accumulator (csrc/engine.hip run_block / run_block_out)
+            b_ = z.shape[0]
+            W1 = torch.cat([w["W_Q"].permute(1, 0, 2).reshape(d, H * dh), w["W_K"].permute(1, 0, 2).reshape(d, H * dh),
+                            w["W_V"].permute(1, 0, 2).reshape(d, H * dh), w["W_in"]], 1)
+            y = self.acc_matmul(xv.reshape(b_ * T, d), W1, splits=acc[1]).reshape(b_, T, -1)
+            qa = self._rotate((y[..., :d].reshape(b_, T, H, dh) + w["b_Q"]).float().double())
+            ka = self._rotate((y[..., d:2 * d].reshape(b_, T, H, dh) + w["b_K"]).float().double())
+            va = (y[..., 2 * d:3 * d].reshape(b_, T, H, dh) + w["b_V"]).float().double()
+            sc = torch.einsum("bqhe,bkhe->bhqk", qa, ka) / math.sqrt(dh)
+            za = torch.einsum("bkhe,bhqk->bqhe", va, torch.softmax(sc.masked_fill(mask, float("-inf")), dim=-1))
+            za = self.R("a_z", za.float().double())
+            ga = self.R("a_gelu", torch.nn.functional.gelu((y[..., 3 * d:] + w["b_in"]).float().double()).float().double())
+            W2 = torch.cat([w["W_O"].reshape(H * dh, d), w["W_out"]], 0)
+            o = self.acc_matmul(torch.cat([za.reshape(b_, T, H * dh), ga], -1).reshape(b_ * T, -1), W2,
+                                splits=acc[0]).reshape(b_, T, d)
+            res_last = torch.einsum("bhe,hed->bhd", za[:, -1], w["W_O"]) if want_result_last else None
+            return (resid + (o + (w["b_O"] + w["b_out"]))).float().double(), res_last
         attn = self.R("gemm_out", zo.reshape(z.shape[0], T, H * dh) @ w["W_O"].reshape(H * dh, d))
         if replace:
             rows = sorted({r for r, _, _ in replace})
@@ -83,8 +103,37 @@ class Rounded(StreamedPythiaOracle):
         res_last = torch.einsum("bhe,hed->bhd", z[:, -1], w["W_O"]) if want_result_last else None
         return self.R("resid", resid + (attn + w["b_O"]) + (mlp + w["b_out"])), res_last
 
+    @staticmethod
+    def _hi(x, scale):
+        return (x * scale).float().half().double() / scale
+
+    def acc_matmul(self, x, w, step=32, splits=1, three=None):
+        """x @ w the way a matrix core accumulates it in fp32 (rule "acc"): products of 32-deep k-slices exact,
+        each slice added to an fp32 accumulator (one rounding per slice), ``splits`` K ranges accumulated
+        separately and summed in fp32 at the end (split-K).  x: [..., K] (already rounded operands)."""
+        K = x.shape[-1]
+        three = self.rules.get("acc3") if three is None else three
+        if three:  # the x2f16 GEMM's three products per slice, small terms first (csrc/gemm_pingpong.hpp)
+            m = w.abs().max().item()
+            sw = 2.0 ** (14 - math.floor(math.log2(m))) if m > 0 else 1.0
+            x0, w0 = self._hi(x, 16.0), self._hi(w, sw)
+            parts = [(x - x0, w0), (x0, w - w0), (x0, w0)]
+        else:
+            parts = [(x, w)]
+        out = None
+        for s in range(splits):
+            k0, k1 = s * K // splits, (s + 1) * K // splits
+            acc = torch.zeros(x.shape[:-1] + (w.shape[-1],), dtype=torch.float32, device=x.device)
+            for k in range(k0, k1, step):
+                for xa, wa in parts:
+                    acc = (acc.double() + xa[..., k:min(k + step, k1)] @ wa[k:min(k + step, k1)]).float()
+            out = acc if out is None else (out.double() + acc.double()).float()
+        return out.double()
+
     def _final_last(self, resid):
         x = self.R("a_u", self._ln_pre(resid[:, -1]))
+        if self.rules.get("acc"):
+            return self.acc_matmul(x, self.R("w_U", self.W_U)) + self.b_U
         return x @ self.R("w_U", self.W_U) + self.b_U
 
 
@@ -158,6 +207,12 @@ def variants():
         v[tag] = dict(v["fp32_all"], **{k: fw for k in WEIGHTS}, **{k: fa for k in ACTS})
         v[tag + "_acts_only"] = {k: fa for k in ACTS}
         v[tag + "_gelu_only"] = {"a_gelu": fa}
+    # plus the matrix cores' fp32 accumulation (32-deep slices, one rounding each; clean forwards only):
+    # the whole K in one accumulator, or the O + MLP-out GEMM split in 2 / 4
+    for sp in (1, 2, 4):
+        v[f"x2e_acc_o{sp}"] = dict(v["x2e"], acc=(sp, 1))
+        v[f"x2e_acc3_o{sp}"] = dict(v["x2e"], acc=(sp, 1), acc3=True)
+    v["fp32_acc"] = dict(v["fp32_all"], acc=(1, 1))
     for k in WEIGHTS + ACTS:  # the engine's bf16 mode with ONE operand group kept exact
         v["engine_bf16_but_" + k] = {kk: vv for kk, vv in eng.items() if kk != k}
     return v

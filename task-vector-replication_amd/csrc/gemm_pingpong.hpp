@@ -80,6 +80,33 @@ constexpr int PP_EPI_LDR = 260;                   // floats per LDS row
 // QKV + MLP-in outputs (qkv fp32, GELU planes: 72 KB per row) stored non-temporal:
 // +2 % on that GEMM (the residual / unembed outputs measured no better); A/B: -DTVR_PP_NT=0
 constexpr bool PP_NT_STORES = TVR_PP_NT;
+// x2f16 sliced accumulation: each 32-deep k-slice's three products (a1 w0, a0 w1, a0 w0) are summed in a
+// fresh MFMA accumulator and added to the tile's accumulator once (one fp32 rounding of the running sum per
+// slice instead of three).  The running sum's roundings are the path's dominant error at large K (Pythia-
+// 12B's O + MLP-out GEMM: K = 25,600 -> 2,400 roundings per output before, 800 now; DESIGN.md §2, the
+// accumulation term of tools/precision_probe.py).  Cost: 4 v_add_f32 per (16x16 tile, k-slice) beside 3
+// MFMAs and a transient 4-VGPR accumulator.  A/B: -DTVR_PP_SLICE_ACC=0.
+#ifndef TVR_PP_SLICE_ACC
+#define TVR_PP_SLICE_ACC 1
+#endif
+constexpr bool PP_SLICE_ACC = TVR_PP_SLICE_ACC;
+// The slice's add as four v_add_f32 (opaque asm: the SLP vectorizer otherwise packs them into v_pk_add_f32,
+// which the guide measures as an anti-lever beside MFMAs); A/B: -DTVR_PP_SLICE_ASM=0.
+#ifndef TVR_PP_SLICE_ASM
+#define TVR_PP_SLICE_ASM 1
+#endif
+__device__ __forceinline__ f32x4 slice_add(f32x4 c, f32x4 t) {
+#if TVR_PP_SLICE_ASM
+  float c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+  asm("v_add_f32 %0, %1, %2" : "=v"(c0) : "v"(c0), "v"(t[0]));
+  asm("v_add_f32 %0, %1, %2" : "=v"(c1) : "v"(c1), "v"(t[1]));
+  asm("v_add_f32 %0, %1, %2" : "=v"(c2) : "v"(c2), "v"(t[2]));
+  asm("v_add_f32 %0, %1, %2" : "=v"(c3) : "v"(c3), "v"(t[3]));
+  return f32x4{c0, c1, c2, c3};
+#else
+  return c + t;
+#endif
+}
 constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
 
 // EPI_STATS: the rows of one LDS half (acc * acc_scale, row stride
@@ -383,7 +410,12 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       for (int j = 0; j < 2; ++j) {
         if (decltype(part)::value && i0 + i >= vi) continue;
         f32x4 c = acc[i0 + i][j0 + j];
-        if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
+        if constexpr (FMT == ACT_X2F16 && PP_SLICE_ACC) {  // the slice's sum first, then one add (see above)
+          f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], t, 0, 0, 0);
+          c = slice_add(c, t);
+        } else if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
