@@ -331,6 +331,9 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
 #define TVR_PP1(E, F, V) \
   hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
                      ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_PP1S(V)                                                                                              \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_RESID, ACT_X2F16, V, 0, false, true>), g, dim3(PP_THREADS), 0, st, \
+                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
 #define TVR_PP1V(E, F) \
   if (vec) { TVR_PP1(E, F, true); } else { TVR_PP1(E, F, false); }
 #define TVR_PP1F(E) \
@@ -345,8 +348,15 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
     case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked)
       if (a_fmt == ACT_X2F16) { TVR_PP1(EPI_STATS, ACT_X2F16, true); } else { TVR_PP1(EPI_STATS, ACT_BF16, true); }
       break;
-    default: TVR_PP1F(EPI_RESID); break;
+    default:
+      if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K) {  // sliced accumulation (gemm_pingpong.hpp)
+        if (vec) { TVR_PP1S(true); } else { TVR_PP1S(false); }
+      } else {
+        TVR_PP1F(EPI_RESID);
+      }
+      break;
   }
+#undef TVR_PP1S
 #undef TVR_PP1F
 #undef TVR_PP1V
 #undef TVR_PP1
@@ -370,7 +380,10 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(count * ksplit), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16)
+  if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K)  // sliced accumulation (gemm_pingpong.hpp)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true>), g, dim3(PP_THREADS), 0, st,
+                       Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_F16)
@@ -412,7 +425,10 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(G), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16)
+  if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K)  // sliced accumulation (gemm_pingpong.hpp)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true, true>), g, dim3(PP_THREADS), 0, st,
+                       Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,
                        (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_F16)

@@ -80,33 +80,22 @@ constexpr int PP_EPI_LDR = 260;                   // floats per LDS row
 // QKV + MLP-in outputs (qkv fp32, GELU planes: 72 KB per row) stored non-temporal:
 // +2 % on that GEMM (the residual / unembed outputs measured no better); A/B: -DTVR_PP_NT=0
 constexpr bool PP_NT_STORES = TVR_PP_NT;
-// x2f16 sliced accumulation: each 32-deep k-slice's three products (a1 w0, a0 w1, a0 w0) are summed in a
-// fresh MFMA accumulator and added to the tile's accumulator once (one fp32 rounding of the running sum per
-// slice instead of three).  The running sum's roundings are the path's dominant error at large K (Pythia-
-// 12B's O + MLP-out GEMM: K = 25,600 -> 2,400 roundings per output before, 800 now; DESIGN.md §2, the
-// accumulation term of tools/precision_probe.py).  Cost: 4 v_add_f32 per (16x16 tile, k-slice) beside 3
-// MFMAs and a transient 4-VGPR accumulator.  A/B: -DTVR_PP_SLICE_ACC=0.
-#ifndef TVR_PP_SLICE_ACC
-#define TVR_PP_SLICE_ACC 1
+// x2f16 sliced accumulation (template SL): each 32-deep k-slice's three products (a1 w0, a0 w1, a0 w0) are
+// summed in a fresh MFMA accumulator and added to the tile's accumulator once (one fp32 rounding of the
+// running sum per slice instead of three).  The running sum's roundings are the path's dominant error at
+// large K (Pythia-12B's O + MLP-out GEMM: K = 25,600 -> 2,400 roundings per output before, 800 now;
+// DESIGN.md §2, the accumulation term of tools/precision_probe.py).  Cost: the extra adds and a transient
+// 4-VGPR accumulator took the GEMMs from 462 to 394 TF/s at C3, so the host asks for it only where K
+// needs it: K >= PP_SLICE_MIN_K (the O + MLP-out GEMM of 6.9B / 12B; not 2.8B's K = 12,800, whose
+// unsliced error is 8e-6 of max |CIE|).  A/B: -DTVR_PP_SLICE_MIN_K=<K>.
+#ifndef TVR_PP_SLICE_MIN_K
+#define TVR_PP_SLICE_MIN_K 16384
 #endif
-constexpr bool PP_SLICE_ACC = TVR_PP_SLICE_ACC;
-// The slice's add as four v_add_f32 (opaque asm: the SLP vectorizer otherwise packs them into v_pk_add_f32,
-// which the guide measures as an anti-lever beside MFMAs); A/B: -DTVR_PP_SLICE_ASM=0.
-#ifndef TVR_PP_SLICE_ASM
-#define TVR_PP_SLICE_ASM 1
-#endif
-__device__ __forceinline__ f32x4 slice_add(f32x4 c, f32x4 t) {
-#if TVR_PP_SLICE_ASM
-  float c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
-  asm("v_add_f32 %0, %1, %2" : "=v"(c0) : "v"(c0), "v"(t[0]));
-  asm("v_add_f32 %0, %1, %2" : "=v"(c1) : "v"(c1), "v"(t[1]));
-  asm("v_add_f32 %0, %1, %2" : "=v"(c2) : "v"(c2), "v"(t[2]));
-  asm("v_add_f32 %0, %1, %2" : "=v"(c3) : "v"(c3), "v"(t[3]));
-  return f32x4{c0, c1, c2, c3};
-#else
-  return c + t;
-#endif
-}
+constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
+// (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
+// read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
+// x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
+__device__ __forceinline__ f32x4 slice_add(f32x4 c, f32x4 t) { return c + t; }
 constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
 
 // EPI_STATS: the rows of one LDS half (acc * acc_scale, row stride
@@ -296,7 +285,7 @@ struct PpLds {
 // tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256 tile
 // (split-K / stream-K), else the launch's fused epilogue.  (A separate int
 // flag: testing the pointer itself made hipcc spill 26-66 VGPRs.)
-template <int EPI, int FMT, bool VEC, int VAR>
+template <int EPI, int FMT, bool VEC, int VAR, bool SL>
 __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda, size_t aps,
                                         const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale, int M,
                                         int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part, int has_part,
@@ -410,7 +399,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       for (int j = 0; j < 2; ++j) {
         if (decltype(part)::value && i0 + i >= vi) continue;
         f32x4 c = acc[i0 + i][j0 + j];
-        if constexpr (FMT == ACT_X2F16 && PP_SLICE_ACC) {  // the slice's sum first, then one add (see above)
+        if constexpr (FMT == ACT_X2F16 && SL) {  // the slice's sum first, then one add (see above)
           f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], t, 0, 0, 0);
@@ -550,8 +539,8 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
 // same instruction stream: timing only).  SKM: the stream-K form (sk_blocks
-// blocks; EPI_BIAS partial tiles only).
-template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false>
+// blocks; EPI_BIAS partial tiles only).  SL: x2f16 sliced accumulation (above).
+template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false, bool SL = false>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
                      size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
@@ -586,7 +575,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       const int nk = (int)min((long long)(nk_all - kbeg), it1 - it);
       int m0, n0;
       pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-      pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+      pp_tile<EPI, FMT, VEC, VAR, SL>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                   ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, 1, st0, sr0);
       it += nk;
     };
@@ -602,7 +591,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
     const int kbeg = (int)((long long)split * nk_all / S);
     const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
-    pp_tile<EPI, FMT, VEC, VAR>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+    pp_tile<EPI, FMT, VEC, VAR, SL>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                 ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS, S > 1, st0, sr0);
   }
 }
