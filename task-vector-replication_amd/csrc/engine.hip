@@ -322,41 +322,41 @@ int act_fmt(const tvr_model* m) {
 int pp_group_m(int N) { return (N + 255) / 256 <= 16 ? 2 : 4; }
 
 void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
-               const GemmEpi& ep0, float acc_scale, int tile_base, int count, bool vec, hipStream_t st) {
+               const GemmEpi& ep0, float acc_scale, int tile_base, int count, bool vec, bool sl, hipStream_t st) {
   GemmEpi ep = ep0;
   ep.tile_base = tile_base;
   ep.tile_count = count;
   ep.group_m = pp_group_m(N);
   const dim3 g(count > 0 ? count : gemm_pingpong_grid(M, N));
-#define TVR_PP1(E, F, V) \
-  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda, (size_t)lda, W.h, \
-                     ldw, W.wps, acc_scale, M, N, K, ep)
-#define TVR_PP1S(V)                                                                                              \
-  hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_RESID, ACT_X2F16, V, 0, false, true>), g, dim3(PP_THREADS), 0, st, \
-                     Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
-#define TVR_PP1V(E, F) \
-  if (vec) { TVR_PP1(E, F, true); } else { TVR_PP1(E, F, false); }
-#define TVR_PP1F(E) \
-  if (a_fmt == ACT_X2F16) { TVR_PP1V(E, ACT_X2F16); } else { TVR_PP1V(E, ACT_BF16); }
+#define TVR_PP1(E, F, V, S)                                                                                       \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V, 0, false, S>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,       \
+                     (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
+#define TVR_PP1V(E, F, S) \
+  if (vec) { TVR_PP1(E, F, true, S); } else { TVR_PP1(E, F, false, S); }
+#define TVR_PP1F(E)                                                                                \
+  if (a_fmt == ACT_X2F16) {                                                                        \
+    if (sl) { TVR_PP1V(E, ACT_X2F16, true); } else { TVR_PP1V(E, ACT_X2F16, false); }             \
+  } else {                                                                                         \
+    TVR_PP1V(E, ACT_BF16, false);                                                                  \
+  }
   if (a_fmt == ACT_F16) {  // the bf16 mode's Q / K columns: plain fp32 outputs only (launch_gemm checks)
-    TVR_PP1V(EPI_BIAS, ACT_F16);
+    TVR_PP1V(EPI_BIAS, ACT_F16, false);
     return;
   }
   switch (epi) {
     case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
     case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
     case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked)
-      if (a_fmt == ACT_X2F16) { TVR_PP1(EPI_STATS, ACT_X2F16, true); } else { TVR_PP1(EPI_STATS, ACT_BF16, true); }
-      break;
-    default:
-      if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K) {  // sliced accumulation (gemm_pingpong.hpp)
-        if (vec) { TVR_PP1S(true); } else { TVR_PP1S(false); }
+      if (a_fmt != ACT_X2F16) {
+        TVR_PP1(EPI_STATS, ACT_BF16, true, false);
+      } else if (sl) {
+        TVR_PP1(EPI_STATS, ACT_X2F16, true, true);
       } else {
-        TVR_PP1F(EPI_RESID);
+        TVR_PP1(EPI_STATS, ACT_X2F16, true, false);
       }
       break;
+    default: TVR_PP1F(EPI_RESID); break;
   }
-#undef TVR_PP1S
 #undef TVR_PP1F
 #undef TVR_PP1V
 #undef TVR_PP1
@@ -366,7 +366,7 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
 // tiles to the model's split-K workspace, then splitk_reduce_kernel sums them
 // in order and applies the epilogue (deterministic).
 int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
-                     const GemmEpi& ep0, float acc_scale, int tile_base, int count, int ksplit, tvr_model* m,
+                     const GemmEpi& ep0, float acc_scale, int tile_base, int count, int ksplit, bool sl, tvr_model* m,
                      hipStream_t st) {
   const int rc = ensure_splitk(m, (size_t)ksplit * count * PP_TILE_ELEMS * sizeof(float), st);
   if (rc != TVR_OK) return rc;
@@ -380,7 +380,7 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(count * ksplit), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K)  // sliced accumulation (gemm_pingpong.hpp)
+  if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true>), g, dim3(PP_THREADS), 0, st,
                        Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_X2F16)
@@ -412,7 +412,8 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
 // the model's split-K workspace, then splitk_sk_reduce_kernel sums each tile's
 // partials in k order and applies the epilogue (deterministic).
 int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
-                 const GemmEpi& ep0, float acc_scale, int tile_base, int count, int G, tvr_model* m, hipStream_t st) {
+                 const GemmEpi& ep0, float acc_scale, int tile_base, int count, int G, bool sl, tvr_model* m,
+                 hipStream_t st) {
   const int rc = ensure_splitk(m, (size_t)2 * G * PP_TILE_ELEMS * sizeof(float), st);
   if (rc != TVR_OK) return rc;
   GemmEpi ep = ep0;
@@ -425,7 +426,7 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(G), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16 && K >= PP_SLICE_MIN_K)  // sliced accumulation (gemm_pingpong.hpp)
+  if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true, true>), g, dim3(PP_THREADS), 0, st,
                        Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_X2F16)
@@ -635,6 +636,9 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   if (planar) {
     const uint16_t* Ah = static_cast<const uint16_t*>(A);
     const bool vec = planar_epilogue_vec(epi, ep, N);
+    // x2f16 sliced accumulation (gemm_pingpong.hpp) on every GEMM of a model whose O + MLP-out K reaches
+    // PP_SLICE_MIN_K (6.9B, 12B), or on any launch of that K
+    const bool sl = a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (m && m->K2 >= PP_SLICE_MIN_K));
     if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec &&
         a_fmt != ACT_F16) {
       // a few rows (the linearised entry's G on a rank of a head split): gemm_skinny.hpp
@@ -656,18 +660,19 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
       PpPlan plan;
       if (m && vec && epi != EPI_STATS) plan = plan_pp_cached(m, M, N, K, a_fmt, epi);
       if (plan.sk_base >= 0) {
-        if (plan.sk_base > 0) launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.sk_base, true, st);
+        if (plan.sk_base > 0)
+          launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.sk_base, true, sl, st);
         TVR_TRY(launch_pp_sk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.sk_base,
-                             gemm_pingpong_grid(M, N) - plan.sk_base, plan.sk_blocks, m, st));
+                             gemm_pingpong_grid(M, N) - plan.sk_base, plan.sk_blocks, sl, m, st));
       } else if (plan.ksplit > 1) {
         TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, gemm_pingpong_grid(M, N),
-                                 plan.ksplit, m, st));
+                                 plan.ksplit, sl, m, st));
       } else if (plan.tail_base > 0) {
-        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, true, st);
+        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.tail_base, true, sl, st);
         TVR_TRY(launch_pp_splitk(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, plan.tail_base,
-                                 gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, m, st));
+                                 gemm_pingpong_grid(M, N) - plan.tail_base, plan.tail_split, sl, m, st));
       } else {
-        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, 0, vec, st);
+        launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, 0, vec, sl, st);
       }
     }
   } else {

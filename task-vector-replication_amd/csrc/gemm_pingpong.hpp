@@ -84,10 +84,13 @@ constexpr bool PP_NT_STORES = TVR_PP_NT;
 // summed in a fresh MFMA accumulator and added to the tile's accumulator once (one fp32 rounding of the
 // running sum per slice instead of three).  The running sum's roundings are the path's dominant error at
 // large K (Pythia-12B's O + MLP-out GEMM: K = 25,600 -> 2,400 roundings per output before, 800 now;
-// DESIGN.md §2, the accumulation term of tools/precision_probe.py).  Cost: the extra adds and a transient
-// 4-VGPR accumulator took the GEMMs from 462 to 394 TF/s at C3, so the host asks for it only where K
-// needs it: K >= PP_SLICE_MIN_K (the O + MLP-out GEMM of 6.9B / 12B; not 2.8B's K = 12,800, whose
-// unsliced error is 8e-6 of max |CIE|).  A/B: -DTVR_PP_SLICE_MIN_K=<K>.
+// DESIGN.md §2, the accumulation term of tools/precision_probe.py).  Cost: 8 adds (20 VALU instructions)
+// per 24 MFMAs: 454 -> 399 TF/s on the C3 GEMMs with every launch sliced (r04i; 394 with the adds placed
+// by the compiler, 363 with them after the cluster; summing only the two small products in t and the big
+// one straight into the tile sum: 401 TF/s but 12B at 6.8e-5 instead of 3.8e-5 of max |CIE|).  So the
+// host asks for it only where the fp32 bar needs it: every x2f16 GEMM of a model whose O + MLP-out K
+// reaches PP_SLICE_MIN_K (6.9B, 12B: slicing that GEMM alone left 12B at 0.99e-4 of max |CIE|, all of
+// them 0.38e-4); 2.8B (K = 12,800) runs unsliced at 0.36e-4.  A/B: -DTVR_PP_SLICE_MIN_K=<K>.
 #ifndef TVR_PP_SLICE_MIN_K
 #define TVR_PP_SLICE_MIN_K 16384
 #endif
@@ -393,6 +396,32 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
   };
   auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part) {
+    if constexpr (FMT == ACT_X2F16 && SL && !decltype(part)::value) {
+      // sliced, all 8 tiles live: tile pairs (i, 0..1) in turn — the pair's first products, second, third
+      // (two independent chains back to back) — and each pair's two slice sums added to the tile
+      // accumulators while the NEXT pair's MFMAs run (sched_group_barrier pins that interleave: 6 MFMAs,
+      // then the pair's 5 adds), so the adds find their MFMA results complete instead of waiting in s_nops
+      f32x4 t[4][2];
+#pragma unroll
+      for (int i = 0; i <= 4; ++i) {
+        if (i < 4) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t[i][j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], t[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        }
+        if (i > 0) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i0 + i - 1][j0 + j] = slice_add(acc[i0 + i - 1][j0 + j], t[i - 1][j]);
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
