@@ -28,7 +28,10 @@
 
 namespace tvr {
 
-constexpr int ENTRY_GROUP = 16;  // sites of one head per block: W_O[h] read once for them
+#ifndef TVR_ENTRY_GROUP
+#define TVR_ENTRY_GROUP 16
+#endif
+constexpr int ENTRY_GROUP = TVR_ENTRY_GROUP;  // sites of one head per block: W_O[h] read once for them
 
 template <int DH>
 __global__ void __launch_bounds__(ENTRY_THREADS)
