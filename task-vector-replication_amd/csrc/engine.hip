@@ -319,7 +319,15 @@ int act_fmt(const tvr_model* m) {
 // there are at most 16 block columns (tools/gemm_split_probe x2ppgm<N>: at
 // M = 90,000 the qkv shape ran 459 / 451 / 419 TF at 4 / 8 / 16, the
 // MLP-out shape (10 columns) 470 / 466 / 458 at 2 / 4 / 8).
-int pp_group_m(int N) { return (N + 255) / 256 <= 16 ? 2 : 4; }
+// A/B knobs TVR_PP_GM_SMALL / TVR_PP_GM_LARGE (read once) override the two values.
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+int pp_group_m(int N) {
+  static const int small = env_int("TVR_PP_GM_SMALL", 2), large = env_int("TVR_PP_GM_LARGE", 4);
+  return (N + 255) / 256 <= 16 ? small : large;
+}
 
 void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, int ldw, int M, int N, int K,
                const GemmEpi& ep0, float acc_scale, int tile_base, int count, bool vec, bool sl, hipStream_t st) {
@@ -1909,7 +1917,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     ents[k] = e;
   }
   // entry layers' head-replacement sites grouped by head, at most ENTRY_GROUP per
-  // group (entry_mfma.hpp); ent_other: the layer has sites of other kinds (entry_kernel)
+  // group, groups of one head balanced (entry_mfma.hpp); ent_other: the layer has sites of other kinds (entry_kernel)
   std::vector<char> ent_other(L + 1, 0);
   std::vector<int32_t> egidx;
   std::vector<int2> egroups;
@@ -1923,12 +1931,14 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
       else
         ent_other[l] = 1;
     }
-    for (const auto& hv : byhead)
-      for (size_t a = 0; a < hv.second.size(); a += ENTRY_GROUP) {
-        const size_t b = std::min(hv.second.size(), a + (size_t)ENTRY_GROUP);
+    for (const auto& hv : byhead) {  // ceil(n / ENTRY_GROUP) groups of balanced size (the launch ends with its
+      const size_t n = hv.second.size(), ng = (n + ENTRY_GROUP - 1) / ENTRY_GROUP;  // largest group)
+      for (size_t gi = 0; gi < ng; ++gi) {
+        const size_t a = gi * n / ng, b = (gi + 1) * n / ng;
         egroups.push_back(make_int2((int)egidx.size(), (int)(b - a)));
         egidx.insert(egidx.end(), hv.second.begin() + a, hv.second.begin() + b);
       }
+    }
     eg_cnt[l] = (int)egroups.size() - eg_beg[l];
   }
   // algorithmic bytes of each layer's entry launch (profiling): the clean rows

@@ -29,7 +29,7 @@
 namespace tvr {
 
 #ifndef TVR_ENTRY_GROUP
-#define TVR_ENTRY_GROUP 16
+#define TVR_ENTRY_GROUP 4
 #endif
 constexpr int ENTRY_GROUP = TVR_ENTRY_GROUP;  // sites of one head per block: W_O[h] read once for them
 
