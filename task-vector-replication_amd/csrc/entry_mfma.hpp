@@ -10,8 +10,15 @@
 // Grid = (groups, ceil(d / 256)), 4 waves of 64 columns each; a group is up to
 // ENTRY_GROUP sites of one head (the host groups a layer's REPLACE_HEAD entries),
 // whose W_O[h] columns the wave reads once into registers: the launch was bound
-// by re-reading the 80 KB W_O slice of a 256-column block for every site (at
-// C3 a layer's 12 prompts x 32 heads: 12 sites per head, one group).  The
+// by re-reading the 80 KB W_O slice of a 256-column block for every site.  But
+// a group's sites run one after another in its block, so a few large groups
+// leave the chip latency-bound: at C3 (a layer's 12 prompts x 32 heads: 12
+// sites per head) groups of 12 / 8+4 / 4+4+4 ran 76 / 88 / 63 us per launch
+// (r04m, same box); the host splits a head's sites into ceil(n / ENTRY_GROUP)
+// groups of balanced size (the re-reads of W_O[h] come from L2).  (Software-
+// pipelining a group's tiles — the next z tile loaded to registers during this
+// tile's MFMAs, double-buffered LDS, one barrier per tile — ran 78 us against
+// 64 us, same box r04p: not kept.)  The
 // MFMA's k index is a permutation applied to both operands: lane group g
 // supplies k = g CH + j at k-step j (CH = dh / 4), so a lane's A operand is CH
 // consecutive floats of one W_O row (float4 loads) and its B operand CH
