@@ -86,7 +86,8 @@ constexpr bool PP_NT_STORES = TVR_PP_NT;
 // large K (Pythia-12B's O + MLP-out GEMM: K = 25,600 -> 2,400 roundings per output before, 800 now;
 // DESIGN.md §2, the accumulation term of tools/precision_probe.py).  Cost: 8 adds (20 VALU instructions)
 // per 24 MFMAs: 454 -> 399 TF/s on the C3 GEMMs with every launch sliced (r04i; 394 with the adds placed
-// by the compiler, 363 with them after the cluster; summing only the two small products in t and the big
+// by the compiler, 363 with them after the cluster, 396 with a finer 2 MFMA / 2 VALU interleave, 403 with
+// no sched_group_barrier (r04r); summing only the two small products in t and the big
 // one straight into the tile sum: 401 TF/s but 12B at 6.8e-5 instead of 3.8e-5 of max |CIE|).  So the
 // host asks for it only where the fp32 bar needs it: every x2f16 GEMM of a model whose O + MLP-out K
 // reaches PP_SLICE_MIN_K (6.9B, 12B: slicing that GEMM alone left 12B at 0.99e-4 of max |CIE|, all of
