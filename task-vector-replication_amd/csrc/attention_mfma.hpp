@@ -56,6 +56,9 @@ constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 // read from LDS in the MFMA layout.  No block barrier: each wave owns its
 // region and waits for its own DMAs (vmcnt).
 // STAGE 2: K and V only (Q loaded directly; 2/3 of the LDS, so 3 blocks per CU).
+// STAGE 3 (NKT == 2: 16 < T <= 32, the C4 / 6.9B sweeps): V's 32 rows only, as
+// one packed [32][DH] image DMA'd before Q and K are loaded; the PV MFMAs read
+// it from LDS instead of 4-B global loads issued after the softmax.
 template <int FMT, int DH, int NKT, int STAGE = 0>
 __global__ void __launch_bounds__(64 * ATTM_WAVES, STAGE == 1 ? 2 : STAGE == 2 ? 3 : (DH <= 80 && NKT == 1) ? 4 : (DH <= 80 && NKT <= 4 && NKT > 0) ? 3 : 2)
 attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
@@ -69,9 +72,10 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   constexpr bool LONG = NKT == 0;
   constexpr int MAXKT = LONG ? 8 : NKT;
   static_assert(DH % 16 == 0 && DH <= 128 && MAXKT * 16 <= ATT_MAX_T, "d_head / key tiles");
-  static_assert(STAGE == 0 || NKT == 1, "LDS staging: one key tile");
+  static_assert(STAGE == 0 || (STAGE <= 2 && NKT == 1) || (STAGE == 3 && NKT == 2), "LDS staging: key tiles");
   constexpr int SMAT = 16 * DH;  // floats of one staged [16][DH] matrix
-  constexpr int NMAT = STAGE == 1 ? 3 : 2, KOFF = STAGE == 1 ? SMAT : 0;  // staged matrices; K's offset
+  // staged matrices (STAGE 3: V's two key tiles); K's offset
+  constexpr int NMAT = STAGE == 1 ? 3 : 2, KOFF = STAGE == 1 ? SMAT : 0;
   __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * NMAT * SMAT : 4];
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
@@ -111,7 +115,15 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   };
 
   float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * NMAT * SMAT : 0);
-  if constexpr (STAGE != 0) {
+  if constexpr (STAGE == 3) {
+    // V's rows 0 .. 31 (clamped to T - 1) as a packed [32][DH] image, issued before Q and K are loaded so
+    // its latency hides behind theirs and the QK^T / softmax; waited for (vmcnt) before the first PV MFMA
+#pragma unroll
+    for (int i = 0; i < DH / 8; ++i) {
+      const int id = i * 64 + lane, row = id / CH, c = id - row * CH;
+      glds16(row_of(min(row, T - 1)) + 2 * d + h * DH + 4 * c, stg + i * 256);
+    }
+  } else if constexpr (STAGE != 0) {
     // rows: Q = the query tile's rows (padding repeats the last), K / V = keys 0 .. 15 (clamped to T - 1);
     // instruction i of matrix m moves chunks 64 i + lane = (row, c) of the packed image
 #pragma unroll
@@ -234,7 +246,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         if (kt < nkt) {
           const int kj = min(16 * kt + li, T - 1);
           float kf[CH];
-          if constexpr (STAGE != 0)
+          if constexpr (STAGE == 1 || STAGE == 2)
             load_chunk(stg + KOFF + li * DH, kj, kf);  // staged row li = key min(li, T - 1)
           else
             load_chunk(row_of(kj) + d + h * DH, kj, kf);
@@ -283,6 +295,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         for (int r = 0; r < 4; ++r) st[kt][r] = st[kt][r] / sum;
       }
 
+      if constexpr (STAGE == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // V's image has landed
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -294,6 +307,11 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
 #pragma unroll
               for (int dt = 0; dt < NDT; ++dt)
                 zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vpre[r][dt], st[kt][r], zt[dt], 0, 0, 0);
+            } else if constexpr (STAGE == 3) {
+              const float* vr = stg + (16 * kt + 4 * g + r) * DH + li;  // staged row = key min(., T - 1)
+#pragma unroll
+              for (int dt = 0; dt < NDT; ++dt)
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
             } else {
               const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
 #pragma unroll
@@ -305,7 +323,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (STAGE != 0) {
+    if constexpr (STAGE == 1 || STAGE == 2) {
       // z through the wave's first staged region (Q or K: read above): then each lane stores 8 consecutive dims of one
       // row (one 16-B store per plane), so a row's DH dims leave as one contiguous run per plane
 #pragma unroll

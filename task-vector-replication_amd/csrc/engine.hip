@@ -937,6 +937,8 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   // well, 0 loads directly (A/B: profiles/r03/attention_stage_ab.txt)
   const char* se = getenv("TVR_ATT_STAGE");
   const int stage = se && std::string(se) == "0" ? 0 : se && std::string(se) == "1" ? 1 : 2;
+  // two key tiles: V staged through LDS (STAGE 3); TVR_ATT_VSTAGE=0 loads it directly (A/B)
+  static const bool vstage = env_flag("TVR_ATT_VSTAGE");
 #define TVR_ATTM(F, DHV, NK, ...)                                                                                   \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK __VA_OPT__(,) __VA_ARGS__>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
@@ -945,6 +947,7 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   if (nkt == 1 && stage == 1) TVR_ATTM(F, DHV, 1, (DHV <= 80 ? 1 : 0)); /* d_head 128: 98 KB, not staged */ \
   else if (nkt == 1 && stage == 2) TVR_ATTM(F, DHV, 1, (DHV <= 80 ? 2 : 0));                  \
   else if (nkt == 1) TVR_ATTM(F, DHV, 1);                                                       \
+  else if (nkt == 2 && vstage) TVR_ATTM(F, DHV, 2, 3);                                          \
   else if (nkt == 2) TVR_ATTM(F, DHV, 2);                                                       \
   else if (nkt == 4) TVR_ATTM(F, DHV, 4);                                                       \
   else if (nkt == 8) TVR_ATTM(F, DHV, 8);                                                       \
