@@ -550,7 +550,8 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi) {
   if (tiles <= 1024) {
     const PlanCost pc{kt_us, 3.0, epi == EPI_SPLIT_GELU_ACT ? 15.0 : 10.0, 7.0};
     double best = plan_sim(M, N, nkt, 0, tiles, 1, pc);
-    for (int S = 2; S <= 16 && nkt / S >= 8 && tiles * S <= 8192; ++S) {
+    // at most 4,096 partial tiles (1 GiB of split-K workspace, which only grows: ensure_splitk)
+    for (int S = 2; S <= 16 && nkt / S >= 8 && tiles * S <= 4096; ++S) {
       const double c = plan_sim(M, N, nkt, 0, tiles, S, pc) + plan_reduce_us(M, N, 0, tiles, S);
       if (c < best * 0.97) {  // a split must win clearly: the model is approximate
         best = c;
