@@ -39,6 +39,19 @@ def test_pmc_summary_keyed_on_family_and_workload():
     assert bench.pmc_summary("x2f16", "another workload") == (None, None)
 
 
+def test_pmc_summary_c4_any_prompt_length():
+    """The C4 block reads the bf16 counters of the same sweep (model, sites,
+    prompts, shots) at another prompt length; another model never matches."""
+    p = bench.ROOT / "profiles" / "pmc_gemm_bf16.json"
+    d = json.loads(p.read_text())
+    base = d["workload"].rsplit(", T=", 1)[0]
+    assert bench.pmc_summary("bf16", base + ", T=999") == (None, None)  # exact match by default
+    pmc, src = bench.pmc_summary("bf16", base + ", T=999", any_len=True)
+    assert pmc is not None and d["workload"] in src
+    assert bench.pmc_summary("bf16", base.replace("6.9b", "2.8b") + ", T=18", any_len=True) == (None, None)
+    assert bench.pmc_summary("x2f16", base + ", T=18", any_len=True) == (None, None)  # another family
+
+
 def test_hbm_kernels_pmc_traffic_keyed_on_workload():
     """profiles/pmc_hbm_kernels.json (tools/prof_summary.py) attaches memory-side
     bytes per launch to the matching workload's rows only."""
