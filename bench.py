@@ -341,7 +341,8 @@ def config_c4(args, dev, n_tasks=3):
     (one process: the plain functions).  One warm task, then ``n_tasks`` timed
     (tools/bench_configs.py --configs C4 runs the 20-task suite).  Roofline of
     the CIE sweep (95 % of a task's GEMM work): SURVEY §8d's F_alg per site
-    (T = 18) x CIE sites/s against the bf16 dense peak (``site_frac``), and
+    (at the task's prompt length, T = 23) x CIE sites/s against the bf16 dense
+    peak (``site_frac``), and
     the bf16 GEMM family's executed TFLOP/s from a separate profiled CIE pass
     (HIP events on the engine stream), with the committed rocprofv3 PMC
     summary of the same sweep (profiles/pmc_gemm_bf16.json) when its
