@@ -2118,7 +2118,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     ProfSpan ps(m, st);
     const bool mf = eg_cnt[l] > 0 && (c.d_head == 16 || c.d_head == 64 || c.d_head == 80 || c.d_head == 128);
     if (mf) {
-      const dim3 gg(eg_cnt[l], (d + ENTRY_THREADS - 1) / ENTRY_THREADS);
+      const dim3 gg(eg_cnt[l], (d + ENTRY_COLS - 1) / ENTRY_COLS);
       const int32_t* gidx = (const int32_t*)(base + o_egidx);
       const int2* grps = (const int2*)(base + o_egroups) + eg_beg[l];
 #define TVR_ENTRY_MF(DH)                                                                                   \

@@ -7,7 +7,7 @@
 // FMA per (position, column, k) and thread: 1.2 G FMAs per C3 entry layer);
 // here it is a [16 positions x dh] x [dh x 64 columns] tile per wave on
 // v_mfma_f32_16x16x4_f32 (exact fp32 products, as the attention kernel).
-// Grid = (groups, ceil(d / 256)), 4 waves of 64 columns each; a group is up to
+// Grid = (groups, ceil(d / ENTRY_COLS)), 4 waves of 16 ENTRY_NT columns each; a group is up to
 // ENTRY_GROUP sites of one head (the host groups a layer's REPLACE_HEAD entries),
 // whose W_O[h] columns the wave reads once into registers: the launch was bound
 // by re-reading the 80 KB W_O slice of a 256-column block for every site.  But
@@ -39,6 +39,13 @@ namespace tvr {
 #define TVR_ENTRY_GROUP 4
 #endif
 constexpr int ENTRY_GROUP = TVR_ENTRY_GROUP;  // sites of one head per block: W_O[h] read once for them
+// 16-column tiles per wave: 1 (a wave's W_O[h] columns in 20 VGPRs at d_head 80, so more waves per SIMD
+// hide the dependent load chains): 54 / 61 / 66 us per C3 entry launch at 1 / 2 / 4 (r04w, same box)
+#ifndef TVR_ENTRY_NT
+#define TVR_ENTRY_NT 1
+#endif
+constexpr int ENTRY_NT = TVR_ENTRY_NT;
+constexpr int ENTRY_COLS = (ENTRY_THREADS / 64) * 16 * ENTRY_NT;   // columns per block
 
 template <int DH>
 __global__ void __launch_bounds__(ENTRY_THREADS)
@@ -54,12 +61,12 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
   const int head = ents[gidx[grp.x]].head;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.y * ENTRY_THREADS + wave * 64;  // this wave's first column
+  const int n0 = blockIdx.y * ENTRY_COLS + wave * 16 * ENTRY_NT;  // this wave's first column
 
   // B operands: W_O row (column c = n0 + 16 nt + li), k = g CH .. g CH + CH - 1
-  float wb[4][CH];
+  float wb[ENTRY_NT][CH];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+  for (int nt = 0; nt < ENTRY_NT; ++nt) {
     const int c = min(n0 + 16 * nt + li, d - 1);
     const float* wr = w2 + (size_t)c * ldw2 + head * DH + g * CH;
 #pragma unroll
@@ -84,9 +91,9 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
       // the clean rows' values and the vector first (no load between the stores below); lane (li, g) owns
       // position li and columns n0 + 16 nt + 4 g .. + 3
       const int pr = min(li, tn - 1);
-      f32x4 sv[4], vc[4];
+      f32x4 sv[ENTRY_NT], vc[ENTRY_NT];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < ENTRY_NT; ++nt) {
         const int c = min(n0 + 16 * nt + 4 * g, d - 4);
         vc[nt] = *(const f32x4*)(vectors + (size_t)e.vec * d + c);
         sv[nt] = *(const f32x4*)(snap + (size_t)(e.src_row + e.p0 + t0 + pr) * d + c);
@@ -97,9 +104,9 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
         const f32x4 v4 = *(const f32x4*)(zt + li * LDZ + g * CH + q);
         za[q] = v4[0]; za[q + 1] = v4[1]; za[q + 2] = v4[2]; za[q + 3] = v4[3];
       }
-      f32x4 acc[4];
+      f32x4 acc[ENTRY_NT];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < ENTRY_NT; ++nt) {
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};  // two chains (dependent-issue latency)
 #pragma unroll
         for (int j = 0; j < CH; j += 2) {
@@ -110,7 +117,7 @@ entry_replace_mfma_kernel(const EntryDesc* __restrict__ ents, const int32_t* __r
       }
       if (li < tn) {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
+        for (int nt = 0; nt < ENTRY_NT; ++nt) {
           const int c = n0 + 16 * nt + 4 * g;
           if (c < d) *(f32x4*)(resid + (size_t)(e.row0 + t0 + li) * d + c) = sv[nt] + (vc[nt] - acc[nt]);
         }
