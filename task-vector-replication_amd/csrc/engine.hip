@@ -528,10 +528,11 @@ double plan_reduce_us(int M, int N, int t0, int cnt, int S) {
   return 4.0 + rows * 4.0 * (2.0 * S + 1.0) / 5.0e6;  // partials written (by the GEMM) + read, output written
 }
 
-PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi) {
+// sliced: the launch runs the x2f16 sliced accumulation (~13 % more per k-tile: gemm_pingpong.hpp)
+PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
   PpPlan p;
   const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_X2F16 ? 32 : 64);
-  const double kt_us = a_fmt == ACT_X2F16 ? 1.9 : 1.3, seg_us = 15.0, epi_us = 10.0;
+  const double kt_us = (a_fmt == ACT_X2F16 ? 1.9 : 1.3) * (sliced ? 1.13 : 1.0), seg_us = 15.0, epi_us = 10.0;
   // stream-K of `cnt` tiles over min(256, iterations) blocks vs one plain round
   auto sk_us = [&](int cnt) {
     const int G = (int)std::min<long long>(256, (long long)cnt * nkt);
@@ -602,7 +603,7 @@ PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi) {
   const PlanKey key{M, N, K, a_fmt, epi == EPI_SPLIT_GELU_ACT ? 1 : 0, sk_enabled() ? 1 : 0};
   auto it = m->plans.find(key);
   if (it != m->plans.end()) return it->second;
-  const PpPlan p = plan_pp(M, N, K, a_fmt, epi);
+  const PpPlan p = plan_pp(M, N, K, a_fmt, epi, a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || m->K2 >= PP_SLICE_MIN_K));
   if (m->plans.size() > 4096) m->plans.clear();
   m->plans.emplace(key, p);
   return p;
