@@ -316,10 +316,14 @@ int tvr_profile_read_hbm(tvr_model* model, tvr_hbm_stats* out);
  * (gemm_pingpong_kernel, 256 x 256 tiles; engine.hip plan_pp): out[0] k-split
  * of the whole launch, out[1] first tile of a split tail (0: none), out[2] the
  * tail's split, out[3] first stream-K tile (-1: none), out[4] stream-K blocks.
- * gemm_mode: TVR_GEMM_X2F16 or TVR_GEMM_BF16; gelu != 0: the QKV + MLP-in
- * launch (GELU epilogue).  Host-only, no device call (diagnostics, CPU tests).
- * (ABI 10) */
-int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t gelu, int32_t* out);
+ * gemm_mode: TVR_GEMM_X2F16 or TVR_GEMM_BF16; flags bit 0 (TVR_PLAN_GELU):
+ * the QKV + MLP-in launch (GELU epilogue); bit 1 (TVR_PLAN_MODEL_SLICED): the
+ * launch belongs to a model whose O + MLP-out K reaches the sliced-accumulation
+ * threshold (6.9B, 12B: every x2f16 GEMM of such a model runs sliced, as does
+ * any launch with K >= that threshold).  Host-only, no device call
+ * (diagnostics, CPU tests).  (ABI 10; flag bit 1 from round 5) */
+enum { TVR_PLAN_GELU = 1, TVR_PLAN_MODEL_SLICED = 2 };
+int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t flags, int32_t* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);
  * the weight planes of the split / bf16 modes are not included (X3BF16 6 B,

@@ -87,7 +87,14 @@ class Rounded(StreamedPythiaOracle):
             res_last = torch.einsum("bhe,hed->bhd", za[:, -1], w["W_O"]) if want_result_last else None
             return (resid + (o + (w["b_O"] + w["b_out"]))).float().double(), res_last
         attn = self.R("gemm_out", zo.reshape(z.shape[0], T, H * dh) @ w["W_O"].reshape(H * dh, d))
-        if replace:
+        if replace and self.rules.get("entry_engine"):
+            # the engine's REPLACE_HEAD entry (csrc/entry_mfma.hpp): the clean row's attention output as the
+            # rounded GEMM computed it, minus the replaced head's z_h W_O[h] in fp32 operands (the trace's z
+            # and the fp32 W_O), plus the vector — instead of re-summing the other heads' rounded products
+            raw = StreamedPythiaOracle.block(self, l)["W_O"]
+            for r, h, vec in replace:
+                attn[r] = attn[r] - z[r, :, h, :].float().double() @ raw[h].float().double() + vec.to(attn)
+        elif replace:
             rows = sorted({r for r, _, _ in replace})
             ri = torch.tensor(rows, device=x.device)
             result = torch.einsum("bqhe,hed->bqhd", zo[ri], w["W_O"])
@@ -192,6 +199,8 @@ def variants():
     v["all_bf16"] = allbf
     eng = dict(allbf, a_qk=FH, w_W_Q=FH, w_W_K=FH)
     v["engine_bf16"] = eng
+    # + the engine's REPLACE_HEAD entry form (clean attention output - z_h W_O[h] + vector, fp32 operands)
+    v["engine_bf16_entry"] = dict(eng, entry_engine=True)
     v["w_bf16"] = {k: BF for k in WEIGHTS}
     v["act_bf16"] = {k: BF for k in ACTS}
     v["all_f16"] = {k: FH for k in WEIGHTS + ACTS}

@@ -193,6 +193,52 @@ class StreamedPythiaOracle:
         return (acc / len(prompts)).cpu().double()
 
     @torch.no_grad()
+    def layer_sweep(self, seqs: Sequence[Sequence[int]], vector: torch.Tensor, targets: Sequence[int],
+                    layers: Optional[Sequence[int]] = None, k: int = 2):
+        """The layer sweeps of scratch2.py:114-127 / :135-150 on one batch of
+        equal-length prompts: for every (prompt, layer i) a forward with
+        ``hook_attn_out[0, -1] += vector`` at block i (layer_addition_hook,
+        :107-109; the reference's late-binding closure adds the same vector at
+        every layer, App. B1), and the clean forward (:143).  A site row joins
+        the batch at its layer from the clean row's hook_resid_pre — the same
+        numbers as a separate forward from token 0 (the rows before block i are
+        the clean ones).  Returns CPU tensors: clean softmax prob of each
+        target [n], patched prob [n, len(layers)], patched top-k ids
+        [n, len(layers), k] and top-k logits [n, len(layers), k] (the margins)."""
+        cfg = self.cfg
+        L = cfg.n_layers
+        layers = list(range(L)) if layers is None else list(layers)
+        if len({len(s) for s in seqs}) != 1:
+            raise ValueError("layer_sweep: one prompt length per call")
+        n = len(seqs)
+        vec = vector.to(self.device, self.dtype)
+        clean = self._embed(seqs)      # [n, T, d]
+        active = clean[:0]
+        joined: List[Tuple[int, int]] = []  # (prompt, layer) of the site rows, in join order
+        for l in range(L):
+            new = [(i, l) for i in range(n)] if l in layers else []
+            batch = torch.cat([clean, active] + ([clean] if new else []))
+            add = [(n + len(joined) + j, vec) for j in range(len(new))]
+            batch, _ = self._block(l, batch, add_last=add)
+            joined += new
+            clean, active = batch[:n], batch[n:]
+        logits = self._final_last(torch.cat([clean, active]))
+        tg = torch.as_tensor([int(t) for t in targets], device=logits.device)
+        p = torch.softmax(logits, dim=-1)
+        p_clean = p[torch.arange(n, device=p.device), tg].cpu()
+        top = torch.topk(logits[n:], k, dim=-1)
+        p_site = p[n:][torch.arange(len(joined), device=p.device), tg[[i for i, _ in joined]]].cpu()
+        col = {l: c for c, l in enumerate(layers)}
+        P = torch.zeros(n, len(layers), dtype=torch.float64)
+        ids = torch.zeros(n, len(layers), k, dtype=torch.long)
+        vals = torch.zeros(n, len(layers), k, dtype=torch.float64)
+        for j, (i, l) in enumerate(joined):
+            P[i, col[l]] = p_site[j]
+            ids[i, col[l]] = top.indices[j].cpu()
+            vals[i, col[l]] = top.values[j].cpu().double()
+        return p_clean.double(), P, ids, vals
+
+    @torch.no_grad()
     def added_topk(self, seqs: Sequence[Sequence[int]], layer: int, vector: Optional[torch.Tensor], k: int,
                    batch: int = 256) -> torch.Tensor:
         """Top-k ids [n, k] of the last row with ``hook_attn_out[0, -1] += vector``

@@ -764,14 +764,27 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
     if (sc) (void)hipFree(sc);
     if (d_max) (void)hipFree(d_max);
   };
-  // the split-K partials workspace is regrown on demand: release it for a second attempt
+  // The split-K partials workspace is released for a second attempt; the
+  // planes are kept only if that workspace can be re-reserved at its former
+  // size afterwards (the sweep's split-K launches need it back: otherwise they
+  // would fail with NOMEM where the full-GEMM entry succeeds).
+  const size_t splitk_had = m->splitk_bytes;
   for (int attempt = 0;; ++attempt) {
-    if (hipMalloc(&m->lin_planes, (size_t)(L - 2) * npl * per * sizeof(uint16_t)) == hipSuccess &&
-        hipMalloc(&m->lin_c1, (size_t)L * N * sizeof(float)) == hipSuccess &&
-        hipMalloc(&wt, (size_t)d * d * sizeof(float)) == hipSuccess &&
-        hipMalloc(&sc, (size_t)N * d * sizeof(float)) == hipSuccess &&
-        hipMalloc(&d_max, sizeof(unsigned)) == hipSuccess)
-      break;
+    bool ok = hipMalloc(&m->lin_planes, (size_t)(L - 2) * npl * per * sizeof(uint16_t)) == hipSuccess &&
+              hipMalloc(&m->lin_c1, (size_t)L * N * sizeof(float)) == hipSuccess &&
+              hipMalloc(&wt, (size_t)d * d * sizeof(float)) == hipSuccess &&
+              hipMalloc(&sc, (size_t)N * d * sizeof(float)) == hipSuccess &&
+              hipMalloc(&d_max, sizeof(unsigned)) == hipSuccess;
+    if (ok && attempt > 0 && splitk_had > 0) {
+      (void)hipGetLastError();
+      ok = hipMalloc(&m->splitk_ws, splitk_had) == hipSuccess;
+      if (ok) {
+        m->splitk_bytes = splitk_had;
+      } else {
+        m->splitk_ws = nullptr;
+      }
+    }
+    if (ok) break;
     (void)hipGetLastError();
     cleanup();
     wt = sc = nullptr;
@@ -940,7 +953,7 @@ int launch_attention(tvr_model* m, const float* qkv, const float* cache_qkv, con
   const char* se = getenv("TVR_ATT_STAGE");
   const int stage = se && std::string(se) == "0" ? 0 : se && std::string(se) == "1" ? 1 : 2;
   // two key tiles: V staged through LDS (STAGE 3); TVR_ATT_VSTAGE=0 loads it directly (A/B)
-  static const bool vstage = env_flag("TVR_ATT_VSTAGE");
+  const bool vstage = env_flag("TVR_ATT_VSTAGE");  // read per launch, as TVR_ATT_STAGE (in-process A/B tests)
 #define TVR_ATTM(F, DHV, NK, ...)                                                                                   \
   hipLaunchKernelGGL((attention_mfma_kernel<F, DHV, NK __VA_OPT__(,) __VA_ARGS__>), grid, block, 0, st, qkv, 3 * d, cache_qkv, 3 * d, d_seqs, \
                      n_seqs, c.n_heads, z, m->K2, zf, d, zf_last ? 1 : 0, zf_rows, m->range_flag, m->rot_cos, m->rot_sin, d, \
@@ -1346,10 +1359,23 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     }
   }
   std::vector<float> scale(mats.size(), 1.0f);  // sized after the Q / K entries: one per matrix
-  // regression guard (415fc26: scale was once sized before the Q / K entries): one size and one scale per
-  // matrix, and the planes of all of them exactly fill the allocation (checked again after the fill)
-  if (scale.size() != mats.size() || sizes.size() != mats.size())
-    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: plane bookkeeping mismatch");
+  // the planes of every matrix exactly fill the allocation: checked BEFORE any conversion kernel writes
+  // (a fp16 Q / K entry is one plane, every other matrix np planes)
+  size_t planned = 0;
+  for (size_t i = 0; i < mats.size(); ++i) planned += (mats[i] ? (size_t)np : 1) * sizes[i];
+  auto drop_planes = [&]() {
+    (void)hipFree(m->planes);
+    m->planes = nullptr;
+    for (auto& w : m->w1) w = MatW{w.f};
+    for (auto& w : m->w2) w = MatW{w.f};
+    m->w1qk.clear();
+    m->wu = MatW{m->wu.f};
+  };
+  if (planned != total) {
+    drop_planes();
+    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: planes planned " + std::to_string(planned) +
+                                      " != allocated " + std::to_string(total));
+  }
   if (mode == TVR_GEMM_X2F16 || mode == TVR_GEMM_BF16) {
     // one power-of-two scale per matrix from its largest magnitude
     unsigned* d_max = nullptr;
@@ -1401,7 +1427,9 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   }
   if ((size_t)(p - m->planes) != total) {
     (void)hipStreamSynchronize(st);
-    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: planes written " + std::to_string(p - m->planes) +
+    const size_t written = (size_t)(p - m->planes);
+    drop_planes();
+    return fail(TVR_ERR_INTERNAL, "tvr_model_set_gemm: planes written " + std::to_string(written) +
                                       " != allocated " + std::to_string(total));
   }
   TVR_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(unsigned), st));
@@ -1493,13 +1521,14 @@ int tvr_trace_create(tvr_model* m, int32_t max_seqs, int32_t max_tokens, tvr_tra
 
 int tvr_trace_destroy(tvr_trace* t) {
   if (!t) return TVR_OK;
-  // a deferred clean forward still owes its outputs to the caller: run it on
-  // the deferral's stream once everything already queued on any stream (work
-  // sharing the model's workspace included) has finished
+  // a deferred clean forward still owes its outputs to the caller: run it once
+  // everything already queued on any stream (work sharing the model's
+  // workspace included) has finished, on the null stream — the deferral's
+  // stream may already have been destroyed by a C caller
   int rc = TVR_OK;
   if (t->pending) {
     (void)hipDeviceSynchronize();
-    rc = flush_pending(t, t->p_stream);
+    rc = flush_pending(t, nullptr);
   }
   (void)hipDeviceSynchronize();
   if (t->resid) (void)hipFree(t->resid);
@@ -2281,12 +2310,15 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   return TVR_OK;
 }
 
-int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t gelu, int32_t* out) {
-  if (M <= 0 || N <= 0 || K <= 0 || !out || (gemm_mode != TVR_GEMM_X2F16 && gemm_mode != TVR_GEMM_BF16))
+int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t flags, int32_t* out) {
+  if (M <= 0 || N <= 0 || K <= 0 || !out || (gemm_mode != TVR_GEMM_X2F16 && gemm_mode != TVR_GEMM_BF16) ||
+      (flags & ~(TVR_PLAN_GELU | TVR_PLAN_MODEL_SLICED)))
     return fail(TVR_ERR_INVALID, "tvr_gemm_plan: bad argument");
   const int fmt = gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : ACT_BF16;
   if (K % (fmt == ACT_X2F16 ? 32 : 64) != 0) return fail(TVR_ERR_UNSUPPORTED, "tvr_gemm_plan: K not a k-tile multiple");
-  const PpPlan p = plan_pp(M, N, K, fmt, gelu ? EPI_SPLIT_GELU_ACT : EPI_RESID);
+  // the same sliced rule as plan_pp_cached / launch_gemm
+  const bool sliced = fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (flags & TVR_PLAN_MODEL_SLICED));
+  const PpPlan p = plan_pp(M, N, K, fmt, (flags & TVR_PLAN_GELU) ? EPI_SPLIT_GELU_ACT : EPI_RESID, sliced);
   out[0] = p.ksplit;
   out[1] = p.tail_base;
   out[2] = p.tail_split;

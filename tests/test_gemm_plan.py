@@ -21,10 +21,10 @@ D, DMLP = 2560, 10240
 D1, K2 = 3 * D + DMLP, D + DMLP
 
 
-def plan(M, N, K, mode=X2F16, gelu=False):
+def plan(M, N, K, mode=X2F16, gelu=False, model_sliced=False):
     lib = tvr_amd._lib.load()
     out = (ctypes.c_int32 * 5)()
-    assert lib.tvr_gemm_plan(M, N, K, mode, 1 if gelu else 0, out) == 0
+    assert lib.tvr_gemm_plan(M, N, K, mode, (1 if gelu else 0) | (2 if model_sliced else 0), out) == 0
     return {"ksplit": out[0], "tail_base": out[1], "tail_split": out[2], "sk_base": out[3], "sk_blocks": out[4]}
 
 
@@ -80,5 +80,24 @@ def test_bad_arguments():
     assert lib.tvr_gemm_plan(0, D1, D, X2F16, 0, out) == tvr_amd._lib.TVR_ERR_INVALID
     assert lib.tvr_gemm_plan(16, D1, D, 0, 0, out) == tvr_amd._lib.TVR_ERR_INVALID  # f32 has no planar plan
     assert lib.tvr_gemm_plan(16, D1, 100, X2F16, 0, out) == tvr_amd._lib.TVR_ERR_UNSUPPORTED
+    assert lib.tvr_gemm_plan(16, D1, D, X2F16, 4, out) == tvr_amd._lib.TVR_ERR_INVALID  # unknown flag bit
     p = plan(300, 4096 * 3 + 16384, 4096, BF16, True)
     well_formed(p, 300, 4096 * 3 + 16384, 4096, bk=64)
+
+
+# Pythia-12B (C5): every x2f16 GEMM of the model runs the sliced accumulation (its O + MLP-out K = 25,600
+# reaches the threshold), which the planner prices at ~13 % more per k-tile (the host entry point
+# must plan with the same rule as launch_gemm)
+D12, DMLP12 = 5120, 20480
+
+
+@pytest.mark.parametrize("M", [40 * 33, 40 * 33 * 5, 40 * 33 * 17, 40 * 33 * 35 + 12 * 33])
+def test_c5_plans_use_the_sliced_rule(M, monkeypatch):
+    monkeypatch.delenv("TVR_STREAM_K", raising=False)
+    D1_, K2_ = 3 * D12 + DMLP12, D12 + DMLP12
+    q = plan(M, D1_, D12, gelu=True, model_sliced=True)
+    o = plan(M, D12, K2_, model_sliced=True)
+    well_formed(q, M, D1_, D12)
+    well_formed(o, M, D12, K2_)
+    # K >= the threshold is sliced whatever the flag says: the O + MLP-out plan does not depend on it
+    assert plan(M, D12, K2_) == o

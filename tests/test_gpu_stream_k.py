@@ -91,3 +91,71 @@ def test_row_attention_matches_tile_kernel(name, monkeypatch):
     assert (d1 - ref_dp).abs().max().item() <= 1e-4 * ref_dp.abs().max().item() + 1e-7
     assert a1 == R.apply_layered_vectors_to_zero_shot(layered.cpu(), task, arrow, oracle)
     model._check_range("row attention test")
+
+
+def _sweeps(model, prompts, answers, mean, layered, task, arrow):
+    logits = model.forward_clean(prompts, topk=1, return_logits=True)["logits"].cpu().double()
+    dp = tvr_amd.apply_layered_vectors_to_zero_shot_by_probability(layered, task, arrow, model=model)
+    acc = tvr_amd.apply_layered_vectors_to_zero_shot(layered, task, arrow, model=model)
+    cie = tvr_amd.experiments.causal_indirect_effect_sums(mean, prompts, answers, model).cpu().double()
+    return logits, dp.cpu().double(), acc, cie
+
+
+def _ab_against_oracle(name, kshot, env, monkeypatch, n_prompts=3):
+    """The same sweeps with ``env`` = "1" and "0" (an engine A/B switch read per
+    launch), compared with each other and the CPU oracle (the reference's
+    loops): clean logits 1e-5 between forms / 1e-4 vs the oracle, Δprob and
+    CIE 1e-4 of the largest + 1e-7, accuracies identical."""
+    cfg = tvr_amd.get_config(name).with_(n_layers=3)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok)
+    oracle = make_oracle(cfg, sd, tok)
+    task = list(tvr_amd.tasks.letter_to_caps)[:20]
+    arrow = tvr_amd.tasks.ARROW
+    # several prompts share their leading tokens (BOS and, for the CIE, the sites' prefix rows)
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, n_prompts, kshot, seed=1234)
+    answers = [int(t) for t in model.forward_clean(prompts, topk=1)["topk"][:, 0].tolist()]
+    g = torch.Generator().manual_seed(5)
+    mean = (torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g) * 0.5).cuda()
+    layered = tvr_amd.gather_head_activations_to_layers(mean)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv(env, v)
+        out[v] = _sweeps(model, prompts, answers, mean, layered, task, arrow)
+    (l1, d1, a1, c1), (l0, d0, a0, c0) = out["1"], out["0"]
+    assert ((l1 - l0).abs().max() / l0.abs().max()).item() < 1e-5
+    assert (d1 - d0).abs().max().item() <= 1e-4 * d0.abs().max().item() + 1e-7
+    assert a1 == a0
+    assert (c1 - c0).abs().max().item() <= 1e-4 * c0.abs().max().item() + 1e-7
+    ref = torch.stack([oracle.forward(torch.tensor([p]))[0, -1] for p in prompts]).double()
+    assert ((l1 - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    heads = [0, 1, cfg.n_heads - 1]  # the CPU oracle's batch-1 loop on a subset of the heads (time)
+    ref_cie = R.calculate_average_causal_indirect_effect(mean.cpu(), prompts, [[a] for a in answers], oracle,
+                                                         heads=heads).double()[:, heads]
+    c1m = c1[:, heads] / len(prompts)
+    err = (c1m - ref_cie).abs().max().item()
+    print(f"{name} {env} k={kshot} T={len(prompts[0])}: CIE err {err:.2e} of max {ref_cie.abs().max():.2e}")
+    assert err <= 1e-4 * ref_cie.abs().max().item() + 1e-7
+    ref_dp = R.apply_layered_vectors_to_zero_shot_by_probability(layered.cpu(), task, arrow, oracle).double()
+    assert (d1 - ref_dp).abs().max().item() <= 1e-4 * ref_dp.abs().max().item() + 1e-7
+    model._check_range(f"{env} A/B test")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,kshot", [("pythia-2.8b", 5), ("pythia-2.8b", 9), ("pythia-12b", 6)])
+def test_vstage_attention_matches_direct_loads(name, kshot, monkeypatch):
+    """Two-key-tile attention (16 < T <= 32: T = 18 / 30 / 21 here) with V
+    staged through LDS (STAGE 3, TVR_ATT_VSTAGE=1, the default) against V
+    loaded directly (=0), at d_head 80 and 128, including the CIE sweep's
+    shared-prefix (K / V cache) rows — ADVICE r4."""
+    _ab_against_oracle(name, kshot, "TVR_ATT_VSTAGE", monkeypatch)
+
+
+@pytest.mark.timeout(900)
+def test_sliced_split_and_stream_k_at_12b_width(monkeypatch):
+    """Pythia-12B width (O + MLP-out K = 25,600: every x2f16 GEMM of the model
+    runs the sliced accumulation) at small M, so the planner splits: the sliced
+    split-K (TVR_STREAM_K=0) and sliced stream-K (=1) instantiations against
+    each other and the CPU oracle — ADVICE r4."""
+    _ab_against_oracle("pythia-12b", 4, "TVR_STREAM_K", monkeypatch, n_prompts=2)

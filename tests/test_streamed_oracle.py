@@ -118,3 +118,51 @@ def test_rotary_tables_are_the_fp32_references():
     h64 = HookedPythiaOracle(oracle_config(cfg), sd, dtype=torch.float64)
     assert torch.equal(st._sin, h32._sin.double()) and torch.equal(st._cos, h32._cos.double())
     assert not torch.equal(st._sin, h64._sin)
+
+
+def test_layer_sweep_equals_reference_loops(pair):
+    """StreamedPythiaOracle.layer_sweep against the reference's two layer sweeps
+    (scratch2.py:114-127 accuracy, :135-150 Δprob; late-binding closure: the
+    last vector at every layer) run on the whole-model hooked oracle."""
+    cfg, tok, full, streamed, _ = pair
+    r = random.Random(6)
+    xs = [f"<|{r.randrange(100, cfg.d_vocab)}|>" for _ in range(8)]
+    seqs = [[0, tok.encode(x)[0], tok.encode(ARROW)[0]] for x in xs]
+    g = torch.Generator().manual_seed(8)
+    layered = torch.randn(cfg.n_layers, cfg.d_model, generator=g, dtype=torch.float64) * 2
+    # answers: half the clean top-1, half the top-1 with the vector at layer 1 (accuracies neither 0 nor 1)
+    top_clean = streamed.added_topk(seqs, 0, None, 1)[:, 0]
+    top_l1 = streamed.added_topk(seqs, 1, layered[-1], 1)[:, 0]
+    ys = [tok.decode_one(int((top_clean if i % 2 else top_l1)[i])) for i in range(len(xs))]
+    contexts = list(zip(xs, ys))
+    acc_ref = R.apply_layered_vectors_to_zero_shot(layered, contexts, ARROW, full)
+    dp_ref = R.apply_layered_vectors_to_zero_shot_by_probability(layered, contexts, ARROW, full)
+    targets = [tok.encode(y)[0] for y in ys]
+    p0, P, ids, vals = streamed.layer_sweep(seqs, layered[-1], targets)
+    acc = [sum(tok.decode_one(int(ids[i, l, 0])) == ys[i] for i in range(len(xs))) / len(xs)
+           for l in range(cfg.n_layers)]
+    assert acc == acc_ref
+    assert any(0 < a < 1 for a in acc)
+    dp = (P - p0[:, None]).mean(0)
+    assert (dp - dp_ref.double()).abs().max().item() <= 1e-12 * dp_ref.abs().max().item()
+    assert (vals[..., 0] >= vals[..., 1]).all()
+    sub = streamed.layer_sweep(seqs, layered[-1], targets, layers=[2, 0])
+    assert torch.equal(sub[1], P[:, [2, 0]]) and torch.equal(sub[2], ids[:, [2, 0]])
+
+
+def test_rounded_engine_entry_form_is_the_same_cie(pair):
+    """oracle/rounded_pythia.py's ``entry_engine`` rule (the engine's REPLACE_HEAD
+    entry: clean attention output − z_h W_O[h] + vector, fp32 operands) with no
+    operand rounding gives the reference's CIE to fp32 operand precision."""
+    from oracle.rounded_pythia import Rounded
+    cfg, tok, full, streamed, _ = pair
+    emu = Rounded(streamed.cfg, streamed._get, {"entry_engine": True})
+    g = torch.Generator().manual_seed(3)
+    mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, generator=g, dtype=torch.float64)
+    r = random.Random(1)
+    prompts = [[0] + [r.randrange(1, cfg.d_vocab) for _ in range(10)] for _ in range(2)]
+    answers = [int(row.argmax()) for row in streamed.last_logits(prompts)]
+    want = streamed.cie(mean, prompts, answers)
+    got = emu.cie(mean, prompts, answers)
+    assert (got - want).abs().max().item() <= 1e-5 * want.abs().max().item()
+    assert want.abs().max().item() > 1e-3
