@@ -18,8 +18,13 @@ the three-plane bf16 split (``--gemm x3bf16``: 6 products) or
 the fp32 MFMA GEMM's error against fp64 (tests/test_gpu_engine.py,
 profiles/gemm_split_probe_r01.jsonl); ``dtype`` names the emulation.  At N=1
 an ``f32_leg`` re-times the same sweep on the fp32 MFMA path and reports the
-max CIE difference between the two paths, and ``parity`` compares the engine
-with the CPU oracle on the sites the ``cpu_baseline`` leg computes.
+max CIE difference between the two paths; ``parity`` compares the engine with
+the CPU oracle on informative weights (a 4-layer std-0.05 copy at the same
+width: extraction, clean logits and every CIE site of one prompt) and
+``parity_bench_weights`` on the sites the ``cpu_baseline`` leg computes.
+
+``configs``: C2 (N = 1 only: a one-GPU config), C4 and C5 — at N > 1 sharded
+over the ranks as their BASELINE 8-GPU configs say (max-over-ranks times).
 
 Multi-GPU (torchrun, one rank per GPU, RCCL), ``--shard``:
 * ``sites`` (default; BASELINE's C3 "one 32 x 32 sweep sharded across the
@@ -173,8 +178,15 @@ def launch_check(rank: int, world: int, backend: str) -> None:
     dist.all_gather(times, el)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "backend": backend,
-                          "rank_elapsed_s": [t.item() for t in times], "max_elapsed_s": el.item()}), flush=True)
+        w = dist.get_world_size()
+        # the workloads a real run at this world size times (C2 is a one-GPU config: N = 1 only)
+        workloads = {"C3": describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, w, "sites")[0],
+                     "C4": c4_workload(w), "C5": c5_workload(w)}
+        if w == 1:
+            workloads["C2"] = "52 zero-shot prompts (T0=3) x 32 layers"
+        print(json.dumps({"launch_check": True, "n_gpus": w, "backend": backend,
+                          "rank_elapsed_s": [t.item() for t in times], "max_elapsed_s": el.item(),
+                          "workloads": workloads}), flush=True)
     dist.destroy_process_group()
 
 
@@ -299,12 +311,17 @@ def config_c2(model, mean, peak, reps=3):
     return out
 
 
-def config_c5(args, dev, peak):
+def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
     """C5: Pythia-12B, the full 36 x 40 CIE sweep of 12
-    shuffled 10-shot prompts (T = 33): 17,280 patched prompts per step on one
-    GPU (the 8-GPU run shards heads as the headline does).  Seeded synthetic
-    weights and means; one warmup step, `steps` timed.  F_alg per SURVEY §8d."""
+    shuffled 10-shot prompts (T = 33): 17,280 patched prompts per step.  At
+    N > 1 the SAME sweep is split across the ranks as the headline's C3 is
+    (distributed.balanced_site_shard: whole layer pairs per rank, one SUM
+    all-reduce of the [L, H] sums; strong scaling, max-over-ranks time);
+    ``emulate`` times rank 0's share of that split on one GPU.  Seeded
+    synthetic weights and means; one warmup step, ``steps`` timed.  F_alg per
+    SURVEY §8d."""
     import tvr_amd
+    from tvr_amd.distributed import balanced_site_shard
     from tvr_amd.experiments import causal_indirect_effect_sums
     t0 = time.time()
     model = tvr_amd.Model.from_pretrained("pythia-12b", device=dev, seed=0, gemm=args.gemm)
@@ -313,26 +330,70 @@ def config_c5(args, dev, peak):
     mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
     prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, 10, seed=1234)
     build_s = time.time() - t0
-    step = lambda: causal_indirect_effect_sums(mean, prompts, answers, model)  # noqa: E731
+    n_split = emulate or world
+    sites = balanced_site_shard(cfg.n_layers, cfg.n_heads, rank, n_split) if n_split > 1 else None
+
+    def step():
+        cie = causal_indirect_effect_sums(mean, prompts, answers, model, sites=sites)
+        if world > 1:
+            dist.all_reduce(cie)
+        return cie
     step()
     steps = max(1, min(args.steps, 2))
+    if world > 1:
+        dist.barrier()
     with model.range_scope("C5 steps"):  # one range check at the end, as the headline's timed steps
         sec, _ = _sync_time(step, steps)
+    rt = None
+    if world > 1:
+        rt = rank_times(sec, dev)
+        sec = max(rt)
     L, d, V, T = cfg.n_layers, cfg.d_model, cfg.d_vocab, len(prompts[0])
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
     f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
-    units = len(prompts) * L * cfg.n_heads
+    units = len(prompts) * (len(sites) if emulate else L * cfg.n_heads)
     rate = units / sec
+    peak_all = peak * (1 if emulate else world)
     del model
     torch.cuda.empty_cache()
-    return {"workload": f"pythia-12b CIE sweep {L}x{cfg.n_heads} sites, {len(prompts)} prompts/step, 10-shot, T={T}",
+    return {"workload": c5_workload(world, emulate, len(sites) if sites else 0),
+            "n_gpus": world, "scaling": "strong", "rank_elapsed_s": [round(x, 4) for x in rt] if rt else None,
             "units_per_step": units, "steps": steps, "ms_per_step": round(sec * 1e3, 1),
             "value": round(rate, 2), "unit": "patched prompts/s", "gflop_per_site": round(f_alg / 1e9, 2),
-            "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak, 4),
+            "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak_all, 4),
             "model_build_s": round(build_s, 1)}
 
 
-def config_c4(args, dev, n_tasks=3):
+def rank_times(el, dev):
+    """Every rank's elapsed seconds (all_gather), for the max-over-ranks timing of the config legs."""
+    t = torch.tensor([el], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [x.item() for x in out]
+
+
+def c4_workload(world: int) -> str:
+    base = ("pythia-6.9b bf16 FV suite per 50-pair task (answers: the model's zero-shot 2nd / 6th-10th choice, clean "
+            "top-5 accuracy 0.5): extraction 512 x 5-shot, CIE 32x32 over 12 prompts, top-10-head FV added at every "
+            "layer over 50 zero-shot prompts (top-5)")
+    if world > 1:
+        base += (f"; {world} GPUs: extraction prompts contiguous per rank (1 all-reduce), CIE sites in balanced "
+                 "layer-pair blocks per rank (1 all-reduce), injection sites round-robin (1 all-gather)")
+    return base
+
+
+def c5_workload(world: int, emulate: int = 0, n_sites_rank: int = 0) -> str:
+    base = "pythia-12b CIE sweep 36x40 sites, 12 prompts/step, 10-shot, T=33"
+    if emulate:
+        return (f"pythia-12b CIE sweep, rank 0's share of a {emulate}-GPU split (sites in balanced layer-pair blocks "
+                f"per rank: {n_sites_rank} of 1440 sites), 12 prompts/step, 10-shot, T=33 (planning emulation on "
+                "one GPU)")
+    if world > 1:
+        base += ", sites in balanced layer-pair blocks per rank"
+    return base
+
+
+def config_c4(args, dev, n_tasks=3, world=1):
     """C4: Pythia-6.9B in the north star's bf16 configuration,
     the function-vector suite per synthetic 50-pair task — extraction over 512
     five-shot prompts (a1), the 32 x 32 CIE over 12 shuffled prompts (a7), the
@@ -358,13 +419,18 @@ def config_c4(args, dev, n_tasks=3):
     cie_in = {}
 
     def one(ti):
-        # a model-consistent task (answers = the model's own zero-shot top-1 after "x:", as the parity tests'
-        # tasks): random pairs on synthetic weights leave every FV accuracy at 0, this gives the FV a signal
+        # a model-consistent task whose FV accuracy can move both ways: after "x:" the answer is the
+        # model's own zero-shot 2nd choice for even pairs (inside the clean top 5) and its 6th..10th choice for odd
+        # ones (outside it) -- clean top-5 accuracy 0.5; random pairs on synthetic weights would leave it at 0 and
+        # the zero-shot top-1 at 1
         xs = [x for x, _ in tvr_amd.tasks.synthetic_task(50, model.cfg.d_vocab, seed=100 + ti)]
-        top = model.forward_clean([model.to_tokens(x + ":")[0].tolist() for x in xs], topk=1)["topk"][:, 0]
-        task = [(x, model.to_string(int(t))) for x, t in zip(xs, top.tolist())]
+        top = model.forward_clean([model.to_tokens(x + ":")[0].tolist() for x in xs], topk=10)["topk"].tolist()
+        task = [(x, model.to_string(int(t[1] if i % 2 == 0 else t[5 + (i // 2) % 5])))
+                for i, (x, t) in enumerate(zip(xs, top))]
         random.seed(ti)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         t = time.perf_counter()
         ex_prompts = tvr_amd.prompts.sample_icl_prompts(model, task, arrow, ",", 512, 5)
         mean = D.mean_activation_sharded(ex_prompts, model)
@@ -377,24 +443,31 @@ def config_c4(args, dev, n_tasks=3):
         fv = E.assemble_task_vector(mean, cie, 10, 10)
         acc = D.check_accuracy_of_added_task_vector_by_layer_sharded(fv, task, 5, model)
         torch.cuda.synchronize()
-        cie_in.update(mean=mean, prompts=prompts, answers=answers)
-        return time.perf_counter() - t, tc, acc
+        el = time.perf_counter() - t
+        if world > 1:  # the max over ranks (every rank ends with the same all_gather, so they end together)
+            rt = rank_times(el, dev)
+            cie_in["rank_times"] = [round(x, 4) for x in rt]
+            el, tc = max(rt), max(rank_times(tc, dev))
+        cie_in.update(mean=mean, prompts=prompts, answers=answers, task=task)
+        return el, tc, acc
 
     one(0)  # warm: trace / workspace sizing
     runs = [one(ti) for ti in range(1, n_tasks + 1)]
+    clean_acc = E.check_accuracy_of_task_vector(torch.zeros(model.cfg.d_model, device=dev), 0, cie_in["task"], 5,
+                                                model=model)[0]
     cfg = model.cfg
     L, H, d, V = cfg.n_layers, cfg.n_heads, cfg.d_model, cfg.d_vocab
-    # the CIE sweep's roofline: a profiled pass of the last task's sweep
+    # the CIE sweep's roofline: a profiled pass of the last task's sweep (this rank's sites)
     model.profile(True)
-    E.calculate_average_causal_indirect_effect(cie_in["mean"], cie_in["prompts"], cie_in["answers"], model=model)
+    D.cie_sharded(cie_in["mean"], cie_in["prompts"], cie_in["answers"], model)
     torch.cuda.synchronize()
     st = model.profile_stats()
     model.profile(False)
     T = len(model.to_tokens(cie_in["prompts"][0])[0])
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
     f_alg = sum((L - 1 - l) * (2 * P_l * T + 2 * T * (T + 1) * d) + 2 * d * V for l in range(L)) / L
-    cie_rate = sum(12 * L * H / r[1] for r in runs) / n_tasks
-    peak = PEAKS["bf16"]
+    cie_rate = sum(12 * L * H / r[1] for r in runs) / n_tasks  # whole-job rate (all ranks' sites / max time)
+    peak = PEAKS["bf16"] * world
     fam = st["all"]
     gemm_tf = fam["flops"] / (fam["ms"] * 1e-3) / 1e12 if fam["ms"] else None
     workload = f"pythia-6.9b CIE sweep {L}x{H} sites, 12 prompts/step, 5-shot, T={T}"
@@ -405,17 +478,18 @@ def config_c4(args, dev, n_tasks=3):
                 if st[k]["ms"]}
     del model
     torch.cuda.empty_cache()
-    return {"workload": f"pythia-6.9b bf16 FV suite per 50-pair task (answers: the model's zero-shot top-1): "
-                        f"extraction 512 x 5-shot, CIE {L}x{H} over 12 prompts, top-10-head FV added at every layer "
-                        "over 50 zero-shot prompts (top-5)",
+    return {"workload": c4_workload(world),
+            "n_gpus": world, "rank_elapsed_s_last_task": cie_in.get("rank_times"),
             "gemm": "bf16", "tasks_timed": n_tasks, "s_per_task": round(sum(r[0] for r in runs) / n_tasks, 3),
+            "clean_top5_acc_last_task": clean_acc,
             "cie_patched_prompts_per_s": round(cie_rate, 1),
             "cie_roofline": {"workload": workload, "gflop_per_site": round(f_alg / 1e9, 2),
                              "site_tflops": round(cie_rate * f_alg / 1e12, 2),
                              "site_frac": round(cie_rate * f_alg / 1e12 / peak, 4), "peak_tflops": peak,
-                             "peak_basis": "bf16 MFMA dense peak (v_mfma_f32_16x16x32_bf16 / _f16, one product)",
+                             "peak_basis": f"bf16 MFMA dense peak (v_mfma_f32_16x16x32_bf16 / _f16, one product) x "
+                                           f"{world} GPU(s)",
                              "gemm_achieved_tflops": round(gemm_tf, 2) if gemm_tf else None,
-                             "gemm_frac": round(gemm_tf / peak, 4) if gemm_tf else None,
+                             "gemm_frac": round(gemm_tf / PEAKS["bf16"], 4) if gemm_tf else None,
                              "gemm_variants_tflops": variants,
                              "mfma_util_rocprof": (pmc.get("mfma") or {}).get("all") if pmc else None,
                              "mfma_util_variants": {k: v.get("mfma_util") for k, v in
@@ -492,6 +566,64 @@ def cpu_baseline(args, cfg, prompts, answers, mean, model):
     return out, parity
 
 
+def parity_informative(args, dev, cores):
+    """The driver-observed parity number on INFORMATIVE weights:
+    the headline's bench weights (std 0.02) leave |CIE| ~ 1e-6, so ``parity``
+    is measured on a 4-layer Pythia-2.8B-width copy with std-0.05 weights,
+    where one head moves the answer's probability by percents: the CPU oracle
+    (fp32, the reference's loops: scratch2.py:81-100 extraction over 16
+    five-shot prompts, :171-197 CIE over every site of one prompt, answer = the
+    oracle's clean top-1) against the engine on the same seeded weights, prompts
+    and means, on the bench's GEMM path.  Bars as the full-depth tests: CIE
+    |err| <= 1e-4 max|CIE| + 1e-7, extraction / logits 1e-4 relative, top-1
+    identical."""
+    import random
+    import tvr_amd
+    from oracle.hooked_pythia import HookedPythiaOracle, OracleConfig
+    from oracle import reference_experiments as R
+    from tvr_amd.experiments import causal_indirect_effect_sums
+    torch.set_num_threads(cores)
+    t0 = time.time()
+    cfg = tvr_amd.get_config(args.model).with_(n_layers=4)
+    shapes = tvr_amd.weights.hf_param_shapes(cfg)
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, dev, 0.05) for n, s in shapes.items()}
+    model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device=dev, gemm=args.gemm)
+    oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
+                                             cfg.rotary_dim, cfg.n_ctx), sd, tokenizer=model.tokenizer)
+    del sd
+    torch.cuda.empty_cache()
+    task = tvr_amd.tasks.synthetic_task(52, cfg.d_vocab, seed=7)
+    random.seed(11)
+    mean_ref = R.generate_mean_activation(task, tvr_amd.tasks.ARROW, ",", oracle, 16, 5)
+    random.seed(11)
+    mean = tvr_amd.generate_mean_activation(task, tvr_amd.tasks.ARROW, ",", model=model, num_contexts=16,
+                                            len_contexts=5)
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 1, args.kshot, seed=1234)
+    logits_ref = oracle.forward(torch.tensor([prompts[0]]))[0, -1].double()
+    answer = int(logits_ref.argmax())
+    cie_ref = R.calculate_average_causal_indirect_effect(mean_ref, prompts, [[answer]], oracle).double()
+    clean = model.forward_clean(prompts, targets=[answer], topk=1, return_logits=True)
+    cie = causal_indirect_effect_sums(mean_ref.to(dev), prompts, [answer], model).cpu().double()
+    model._check_range("bench parity")
+    cmax = cie_ref.abs().max().item()
+    d_cie = (cie - cie_ref).abs().max().item()
+    out = {"weights": f"{args.model} width, 4 layers, seeded std-0.05 weights (informative: max |CIE| {cmax:.3e})",
+           "sites": cfg.n_layers * cfg.n_heads, "prompt_T": len(prompts[0]), "gemm": args.gemm,
+           "max_abs_cie_err": d_cie, "max_abs_cie_ref": cmax, "max_rel_cie_err": d_cie / max(cmax, 1e-30),
+           "extraction_max_rel_err": ((mean.cpu().double() - mean_ref.double()).abs().max()
+                                      / mean_ref.double().abs().max()).item(),
+           "clean_logits_max_rel_err": ((clean["logits"][0].cpu().double() - logits_ref).abs().max()
+                                        / logits_ref.abs().max()).item(),
+           "top1_equal": int(clean["topk"][0, 0]) == answer,
+           "tolerance": "CIE |err| <= 1e-4 max|CIE| + 1e-7, extraction and logits 1e-4 relative, top-1 identical",
+           "seconds": round(time.time() - t0, 1)}
+    out["ok"] = bool(d_cie <= 1e-4 * cmax + 1e-7 and out["extraction_max_rel_err"] < 1e-4 and
+                     out["clean_logits_max_rel_err"] < 1e-4 and out["top1_equal"] and cmax > 1e-3)
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
 DTYPES = {"x2f16": "f32 (x2f16 emulation: fp32 operands as 2 fp16 planes, 3 MFMA products, fp32 accumulate)",
           "x3bf16": "f32 (x3bf16 emulation: fp32 operands as 3 bf16 planes, 6 MFMA products, fp32 accumulate)",
           "f32": "f32 (v_mfma_f32_32x32x2_f32)",
@@ -511,10 +643,12 @@ def main():
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     if world > 1:
+        # a rank that fails inside a config leg must not leave the others blocked in a collective forever
+        from datetime import timedelta
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timedelta(minutes=10))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=timedelta(minutes=10))
 
     import tvr_amd
     from tvr_amd.distributed import balanced_site_shard, strided_shard
@@ -721,10 +855,20 @@ def main():
             "steps": nw, "value": round(len(prompts) * cfg.n_layers * cfg.n_heads * world * nw / el_w, 2),
             "unit": "patched prompts/s", "scaling": "weak", "rank_elapsed_s": [round(x, 4) for x in rank_times]}
     if rank == 0 and world == 1 and args.cpu_baseline and not emulate:
-        out["cpu_baseline"], out["parity"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
-    which = {c for c in args.configs.split(",") if c} if world == 1 and not emulate and args.model == "pythia-2.8b" \
-        else set()
-    if which:  # the other BASELINE.json configs, timed after the headline (not part of `value`)
+        out["cpu_baseline"], out["parity_bench_weights"] = cpu_baseline(args, cfg, prompts, answers, mean, model)
+        try:
+            out["parity"] = parity_informative(args, dev, out["cpu_baseline"]["cores"])
+        except Exception as e:
+            out["parity"] = {"error": f"{type(e).__name__}: {e}", "ok": False}
+    # the other BASELINE.json configs, timed after the headline (never part of `value`): C2 is a one-GPU config
+    # (N = 1 only); C4 and C5 are BASELINE's 8-GPU configs, sharded over the ranks at N > 1;
+    # --emulate-world times C5's rank-0 share
+    which = {c for c in args.configs.split(",") if c} if args.model == "pythia-2.8b" else set()
+    if world > 1:
+        which -= {"C2"}
+    if emulate:
+        which &= {"C5"}
+    if which:
         out["configs"] = {}
         if "C2" in which:
             try:
@@ -738,13 +882,13 @@ def main():
             model = None
         if "C4" in which:
             try:
-                out["configs"]["C4"] = config_c4(args, dev)
+                out["configs"]["C4"] = config_c4(args, dev, world=world)
                 log(f"C4: {out['configs']['C4']['s_per_task']} s/task")
             except Exception as e:
                 out["configs"]["C4"] = {"error": f"{type(e).__name__}: {e}"}
         if "C5" in which:
             try:
-                out["configs"]["C5"] = config_c5(args, dev, peak)
+                out["configs"]["C5"] = config_c5(args, dev, peak, world, rank, emulate)
                 log(f"C5: {out['configs']['C5']['value']} patched prompts/s")
             except Exception as e:
                 out["configs"]["C5"] = {"error": f"{type(e).__name__}: {e}"}

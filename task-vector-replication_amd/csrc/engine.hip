@@ -688,10 +688,19 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
   } else {
     const float* Af = static_cast<const float*>(A);
     unsigned* flag = m ? m->range_flag : range_flag;
-    const bool large = gemm_use_large(M, N);
-#define TVR_GEMM_LAUNCH(E, TL)                                                                  \
-  hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0, \
-                     st, Af, lda, W.f, ldw, M, N, K, ep)
+    // exact-product fp32 GEMMs of a model whose O + MLP-out K reaches PP_SLICE_MIN_K (6.9B, 12B), or any launch
+    // of that K: the sliced accumulation (gemm_f32.hpp SLICE_KT; the small tile holds the second accumulator set)
+    const bool f32_sliced = !W.h && !W.x && (K >= PP_SLICE_MIN_K || (m && m->K2 >= PP_SLICE_MIN_K));
+    const bool large = gemm_use_large(M, N) && !f32_sliced;
+#define TVR_GEMM_LAUNCH(E, TL)                                                                                    \
+  do {                                                                                                            \
+    if (f32_sliced)                                                                                               \
+      hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TileSmall, F32_SLICE_KT>), dim3(gemm_grid<TileSmall>(M, N)),      \
+                         dim3(TileSmall::THREADS), 0, st, Af, lda, W.f, ldw, M, N, K, ep);                        \
+    else                                                                                                          \
+      hipLaunchKernelGGL((gemm_f32_nt_kernel<E, TL>), dim3(gemm_grid<TL>(M, N)), dim3(TL::THREADS), 0,             \
+                         st, Af, lda, W.f, ldw, M, N, K, ep);                                                     \
+  } while (0)
 #define TVR_X3_LAUNCH(E, TL)                                                                      \
   hipLaunchKernelGGL((gemm_x3bf16_nt_kernel<E, TL>), dim3(gemm_x3_grid<TL>(M, N)), dim3(TL::THREADS), \
                      0, st, Af, lda, W.x, ldw, W.wps, M, N, K, ep)

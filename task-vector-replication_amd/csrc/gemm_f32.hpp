@@ -235,7 +235,18 @@ using TileLarge = GemmTile<256, 256, 2, 4, 32>;
 using TileSmall = GemmTile<128, 128, 2, 2, 32>;
 
 // 2 waves per SIMD for every tile (8 waves per CU).
-template <int EPI, class TL>
+// SLICE_KT > 0 (sliced accumulation, the 6.9B / 12B models: K up to 25,600):
+// the MFMA chain of every SLICE_KT k-tiles (SLICE_KT * 16 fused products per
+// output) runs in a fresh accumulator that is then added to the running sum
+// once — K / (32 SLICE_KT) roundings of the large running sum instead of K / 2
+// (the exact-product chain is one fp32 rounding per product pair); the second
+// accumulator set fits the small tile only (64 + 64 VGPRs), so the host pairs
+// it with TileSmall.  Same idea as gemm_pingpong.hpp's sliced x2f16 form.
+#ifndef TVR_F32_SLICE_KT
+#define TVR_F32_SLICE_KT 4
+#endif
+constexpr int F32_SLICE_KT = TVR_F32_SLICE_KT;  // k-tiles (32 deep) per fresh-accumulator slice
+template <int EPI, class TL, int SLICE_KT = 0>
 __global__ void __launch_bounds__(TL::THREADS, 2)
 gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
                    const float* __restrict__ W, int ldw, int M, int N, int K,
@@ -290,10 +301,17 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
   const int boff = (wc * (BN / TL::WN) + lr) * LDK + lh * 4;
 
   f32x16 acc[TM][TN];
+  f32x16 sum[SLICE_KT > 0 ? TM : 1][SLICE_KT > 0 ? TN : 1];  // the running sum of the sliced form
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+  if constexpr (SLICE_KT > 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) sum[i][j] = f32x16{};
+  }
   f32x4 ra[TL::LOADS_A], rb[TL::LOADS_B];
   f32x4 fa[TM], fb[TN];  // fragments of the k-group being multiplied
 
@@ -358,9 +376,23 @@ gemm_f32_nt_kernel(const float* __restrict__ A, int lda,
       for (int j = 0; j < TN; ++j) fb[j] = nb[j];
     }
     buf ^= 1;
+    if constexpr (SLICE_KT > 0) {
+      if ((kt + 1) % SLICE_KT == 0 || !more) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            sum[i][j] += acc[i][j];
+            acc[i][j] = f32x16{};
+          }
+      }
+    }
   }
 
-  gemm_epilogue<EPI, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lr, lh);
+  if constexpr (SLICE_KT > 0)
+    gemm_epilogue<EPI, TM, TN>(ep, sum, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lr, lh);
+  else
+    gemm_epilogue<EPI, TM, TN>(ep, acc, M, N, m0 + wr * (BM / TL::WM), n0 + wc * (BN / TL::WN), lr, lh);
   if (ep.stamps && t == 0) {
     ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
     ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;

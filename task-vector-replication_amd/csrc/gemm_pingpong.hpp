@@ -96,6 +96,11 @@ constexpr bool PP_NT_STORES = TVR_PP_NT;
 #define TVR_PP_SLICE_MIN_K 16384
 #endif
 constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
+// Placement of the sliced form's adds: 1 (round 5) scalar adds spread over the next pair's MFMA gaps with
+// the last pair carried into the next phase; 0 (round 4) the pair's packed adds after the next pair's MFMAs.
+#ifndef TVR_PP_SLICE_FORM
+#define TVR_PP_SLICE_FORM 1
+#endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
 // x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
@@ -396,12 +401,47 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 #pragma unroll
       for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
   };
-  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part) {
+  // sliced form, all 8 tiles live: the slice sums of the cluster's LAST tile pair are carried into the next
+  // phase's cluster (tc, for acc[ci][cj + 0..1]) and added there, while its first MFMAs run
+  [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part, int ci, int cj) {
     if constexpr (FMT == ACT_X2F16 && SL && !decltype(part)::value) {
-      // sliced, all 8 tiles live: tile pairs (i, 0..1) in turn — the pair's first products, second, third
-      // (two independent chains back to back) — and each pair's two slice sums added to the tile
-      // accumulators while the NEXT pair's MFMAs run (sched_group_barrier pins that interleave: 6 MFMAs,
-      // then the pair's 5 adds), so the adds find their MFMA results complete instead of waiting in s_nops
+#if TVR_PP_SLICE_FORM == 1
+      // tile pairs (i, 0..1) in turn — the pair's first products, second, third (two independent chains back
+      // to back) — and the previous pair's 8 slice-sum adds (the carried pair's for i = 0) spread 2, 2, 1, 1,
+      // 1, 1 over its six MFMA gaps as SCALAR v_add_f32 (the engine builds with -fno-slp-vectorize: packed
+      // v_pk_add_f32 beside MFMAs costs far more than its issue slot, MI355X_MICROARCH.md 'price of one
+      // filler'); two v_add_f32 fit a 16x16x32 gap's free issue cycles, so the adds ride on the MFMA pipe's
+      // time instead of extending the cluster
+      f32x4 t[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int di = i == 0 ? ci : i0 + i - 1, dj = i == 0 ? cj : j0;  // the previous pair's tiles
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int j = q & 1, p = q >> 1;  // MFMA q: product p of tile j (p 0: a1 w0, 1: a0 w1, 2: a0 w0)
+          t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][p == 1 ? 1 : 0], fa[i][p == 0 ? 1 : 0],
+                                                             p == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : t[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          // adds after MFMA q: elements e0 .. e1 of the previous pair's 8 (tile e / 4, element e % 4)
+          const int e0 = q < 2 ? 2 * q : q + 2, e1 = q < 2 ? 2 * q + 2 : q + 3;
+#pragma unroll
+          for (int e = e0; e < e1; ++e)
+            acc[di][dj + (e >> 2)][e & 3] += i == 0 ? tc[e >> 2][e & 3] : t[i - 1][e >> 2][e & 3];
+          if (q < 2)
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          else
+            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+      }
+      tc[0] = t[3][0];
+      tc[1] = t[3][1];
+      return;
+#else
+      // (round-4 form) tile pairs in turn, each pair's two slice sums added while the NEXT pair's MFMAs
+      // run (6 MFMAs, then the pair's adds); the last pair's adds after the cluster
+      (void)ci;
+      (void)cj;
       f32x4 t[4][2];
 #pragma unroll
       for (int i = 0; i <= 4; ++i) {
@@ -422,6 +462,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
         }
       }
       return;
+#endif
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -485,26 +526,33 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       read_w(cur, 0, fwl, part);
       if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
       stage(1, kt + 1);
-      TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part));
+      TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part, 7, 0));  // (ci, cj): the carried pair of the previous phase
       // q2: Q(A_lo, W_hi)
       read_w(cur, 2, fwh, part);
       if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
       stage(3, kt + 1);
-      TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part));
+      TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part, 3, 0));
       // q3: Q(A_hi, W_hi)
       read_a(cur, 4, part);
       stage(0, kt + 2);
-      TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part));
+      TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part, 3, 2));
       // q4: Q(A_hi, W_lo)
       if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
       stage(2, kt + 2);
-      TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part));
+      TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part, 7, 2));
     }
   };
-  if (vi == 8)
+  if (vi == 8) {
     kloop(std::integral_constant<bool, false>{});
-  else
+#if TVR_PP_SLICE_FORM == 1
+    if constexpr (FMT == ACT_X2F16 && SL) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
+      acc[7][0] = slice_add(acc[7][0], tc[0]);
+      acc[7][1] = slice_add(acc[7][1], tc[1]);
+    }
+#endif
+  } else {
     kloop(std::integral_constant<bool, true>{});
+  }
 #undef TVR_PP_CLUSTER
   if constexpr (VAR == 6 || VAR == 8) d_loop1 = __builtin_amdgcn_s_memtime();
   if (wr == 0 && VAR != 3) __builtin_amdgcn_s_barrier();  // balance the group offset

@@ -110,3 +110,28 @@ def test_headline_workload_is_the_strong_c3_sweep():
     # N = 1: the same string whichever --shard was given (the PMC summaries key on it)
     assert bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 1, "prompts") == \
         bench.describe_workload("pythia-2.8b", 32, 32, 12, 4, 15, 1, "heads")
+
+
+def test_launch_check_at_8_ranks_names_every_8gpu_config():
+    """at N = 8 the bench times BASELINE's three multi-GPU configs —
+    C3 (the headline, strong site split), C4 (extraction prompt-sharded, CIE
+    site-sharded, injection round-robin) and C5 (the 12B sweep, strong site
+    split) — and rank 0's launch check reports exactly those workloads."""
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, str(bench.ROOT / "bench.py"), "--gpus", "8", "--dist-backend", "gloo",
+                        "--launch-check"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert out["n_gpus"] == 8 and len(out["rank_elapsed_s"]) == 8
+    w = out["workloads"]
+    assert set(w) == {"C3", "C4", "C5"}
+    assert w["C3"] == ("pythia-2.8b CIE sweep 32x32 sites, 12 prompts/step, 4-shot, T=15, "
+                       "sites in balanced layer-pair blocks per rank")
+    assert w["C5"] == "pythia-12b CIE sweep 36x40 sites, 12 prompts/step, 10-shot, T=33, " \
+                      "sites in balanced layer-pair blocks per rank"
+    assert w["C4"].startswith("pythia-6.9b bf16 FV suite") and "8 GPUs" in w["C4"] and "round-robin" in w["C4"]
+    assert bench.c5_workload(1) == "pythia-12b CIE sweep 36x40 sites, 12 prompts/step, 10-shot, T=33"
