@@ -876,6 +876,7 @@ def main():
                 log(f"C2: {out['configs']['C2']['accuracy']['sites_per_s']} / {out['configs']['C2']['dprob']['sites_per_s']} sites/s")
             except Exception as e:  # a config leg never voids the headline line
                 out["configs"]["C2"] = {"error": f"{type(e).__name__}: {e}"}
+                log(f"[rank {rank}] C2 failed: {out['configs']['C2']['error']}")
         if which & {"C4", "C5"}:
             del model
             torch.cuda.empty_cache()
@@ -886,12 +887,14 @@ def main():
                 log(f"C4: {out['configs']['C4']['s_per_task']} s/task")
             except Exception as e:
                 out["configs"]["C4"] = {"error": f"{type(e).__name__}: {e}"}
+                log(f"[rank {rank}] C4 failed: {out['configs']['C4']['error']}")
         if "C5" in which:
             try:
                 out["configs"]["C5"] = config_c5(args, dev, peak, world, rank, emulate)
                 log(f"C5: {out['configs']['C5']['value']} patched prompts/s")
             except Exception as e:
                 out["configs"]["C5"] = {"error": f"{type(e).__name__}: {e}"}
+                log(f"[rank {rank}] C5 failed: {out['configs']['C5']['error']}")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -232,9 +232,9 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
             assert acc_eng == r["acc_ref"], (acc_eng, r["acc_ref"])
         else:
             # the engine against the bf16-EMULATING fp64 oracle site by site (the engine's operand roundings — bf16,
-            # fp16 Q / K — and its REPLACE_HEAD entry form, everything else fp64): REPORTED at this depth, where two
-            # bf16 implementations that differ at the fp32 level decorrelate (test_c2_layer_sweeps_full_depth_bf16's
-            # docstring); the value-level bar is test_bf16_value_level_shallow's
+            # fp16 Q / K — and its REPLACE_HEAD entry form, everything else fp64); at this depth two bf16
+            # implementations that differ at the fp32 level partly decorrelate (test_bf16_value_level_one_block's
+            # docstring), so the bar is on direction (below), the value-level one is test_bf16_value_level_one_block
             from oracle.rounded_pythia import Rounded, variants
             shapes = tvr_amd.weights.hf_param_shapes(cfg)
             emu = Rounded(oracle_config(cfg), lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", STD),
@@ -255,6 +255,9 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
                   f"top-{FV_HEADS} heads emulation {set_emu} ({len(set(set_emu) & set(set_eng))} shared with the engine)")
             assert e_mean < 2e-2, e_mean
             assert err.max().item() <= 1.5 * floor, (err.max().item(), floor)
+            # direction: the engine's CIE error shares the emulation's (independent errors of that size would put
+            # engine − emulation at ~1.41x the floor; measured 0.55 - 0.66, profiles/r05/gpu_tests_r05d.log)
+            assert e_full <= 1.0 * floor and e_emu <= 1.0 * floor, (e_full, e_emu, floor)
     finally:
         del model
         torch.cuda.empty_cache()
@@ -397,17 +400,20 @@ def test_bf16_value_level_one_block():
     activations, fp16 Q / K — and its REPLACE_HEAD entry form; everything
     else fp64).  Clean last-row logits of 12 prompts, the CIE of every
     (layer 0, head) site over them and the Δprob sweep of 52 prompts: engine −
-    emulation within 0.25x of emulation − fp64, site by site — an engine whose
-    bf16 error points another way than its operand roundings explain fails.
-    Why one block: the engine's fp32 arithmetic (accumulation order, fp32 LN /
+    emulation at most HALF of emulation − fp64 (max over the values): an
+    engine whose bf16 error had the emulation's size but an independent
+    direction would measure sqrt(2) ~ 1.41 there, so one wrong in another
+    direction than its operand roundings explain fails.  Why not closer, and
+    why one block: the engine's fp32 arithmetic (accumulation order, fp32 LN /
     softmax) differs from the emulation's fp64 by ~1e-6 relative, which flips
-    ~0.1 % of the next bf16 roundings; the flips compound block by block
-    (tools/bf16_probe.py, profiles/r05/bf16_probe_r05c.log: engine vs
-    emulation 4 % of the emulation's distance to fp64 after block 0, 21 %
-    after block 1, ~50 % from block 10 on; and 2 / 3-layer truncations measured
-    0.33 / 0.36 on the logits, profiles/r05/gpu_tests_r05d.log), so at depth
-    two correct bf16 implementations decorrelate and the full-depth tests hold
-    bf16 to statistical bars (1.5x the emulated floor)."""
+    a fraction of the next bf16 roundings (each flip is a whole bf16 ulp on
+    that element); the flips compound block by block (tools/bf16_probe.py,
+    profiles/r05/bf16_probe_r05c.log: residual stream engine vs emulation 4 %
+    of the emulation's distance to fp64 after block 0, 21 % after block 1,
+    ~50 % from block 10 on; 2 / 3-layer truncations 0.33 / 0.36 on the logits,
+    profiles/r05/gpu_tests_r05d.log), so at depth two correct bf16
+    implementations decorrelate and the full-depth tests hold bf16 to the
+    1.5x-floor bars."""
     from oracle.rounded_pythia import Rounded, variants
     name = "pythia-6.9b"
     cfg = tvr_amd.get_config(name).with_(n_layers=1)
@@ -446,7 +452,7 @@ def test_bf16_value_level_one_block():
             print(f"bf16 {name} x 1 block, {what}: emulation vs fp64 {floor:.3e} (max |fp64| "
                   f"{refs[i]['f64'].abs().max():.3e}); engine vs emulation {e:.3e} = {e / floor:.3f} of it")
         assert cie["f64"].abs().max().item() > 1e-3
-        assert all(r <= 0.25 for r in ratios), dict(zip(names, ratios))
+        assert all(r <= 0.5 for r in ratios), dict(zip(names, ratios))
     finally:
         del model
         torch.cuda.empty_cache()
