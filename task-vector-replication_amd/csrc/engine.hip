@@ -478,9 +478,15 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
 // stream-K is opt-in: on the C2 sweeps it measured slower than the split-K
 // plan (O + MLP-out 8.2 vs 5.7 ms per sweep) and equal on C3
 // (profiles/r03/c2_stream_k_ab.txt)
-bool sk_enabled() {
+// TVR_STREAM_K: "1" every planned launch, "O" the O + MLP-out launches only (EPI_RESID: 10 column tiles at
+// 2.8B, so a rank's share of a split sweep ends in partly filled rounds), else off
+int sk_mode() {
   const char* e = getenv("TVR_STREAM_K");
-  return e && std::string(e) == "1";
+  return !e ? 0 : std::string(e) == "1" ? 1 : std::string(e) == "O" ? 2 : 0;
+}
+bool sk_enabled(int epi = EPI_BIAS) {
+  const int md = sk_mode();
+  return md == 1 || (md == 2 && epi == EPI_RESID);
 }
 
 struct PlanCost {
@@ -539,7 +545,7 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
     return std::ceil((double)cnt * nkt / G) * kt_us + 2.0 * seg_us + (cnt + 2.0 * G) * 0.0655 + 5.0;
   };
   const double round_plain_us = nkt * kt_us + epi_us;
-  if (sk_enabled() && (long long)tiles * nkt >= 4LL * 256) {
+  if (sk_enabled(epi) && (long long)tiles * nkt >= 4LL * 256) {
     const int rounds = (tiles + 255) / 256;
     const int tb = tiles - 256 * (rounds - 1);  // tiles of the last (partly empty) round
     if (tb < 256 && sk_us(tb) + 5.0 < round_plain_us) {
@@ -600,7 +606,7 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
 // plan_pp, cached per launch shape on the model (the sweeps repeat their
 // per-layer shapes: the simulation runs once per shape)
 PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi) {
-  const PlanKey key{M, N, K, a_fmt, epi == EPI_SPLIT_GELU_ACT ? 1 : 0, sk_enabled() ? 1 : 0};
+  const PlanKey key{M, N, K, a_fmt, epi == EPI_SPLIT_GELU_ACT ? 1 : epi == EPI_RESID ? 2 : 0, sk_mode()};
   auto it = m->plans.find(key);
   if (it != m->plans.end()) return it->second;
   const PpPlan p = plan_pp(M, N, K, a_fmt, epi, a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || m->K2 >= PP_SLICE_MIN_K));
