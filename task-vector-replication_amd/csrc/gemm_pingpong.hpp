@@ -274,7 +274,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
 
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
-// (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
+// (stale LDS: timing only), 2 no s_setprio, 13 s_setprio 1 once for waves 4-7, 14 the cluster flips in the
+// sliced form too, 3 no group offset, 4 no vmcnt
 // waits in the loop (racy: timing only), 6 per-block stamps (start, loop
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
@@ -489,13 +490,17 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
         acc[i0 + i][j0 + j] = c;
       }
   };
-  // [MFMA cluster] between this phase's two barriers
+  // [MFMA cluster] between this phase's two barriers, at s_setprio 1 — except in the sliced form, whose
+  // clusters carry the slice-sum adds: there the flips cost 1.3-1.6 % on the probe's 2.8B-width shapes (370 ->
+  // 375-380 TF/s without them; unsliced within noise either way: profiles/r05/gemm_prio_ab_r05k.jsonl), +0.2 %
+  // (noise) on C5's 12B GEMMs (profiles/r05/c5_prio_ab_r05l.txt)
+  constexpr bool prio = VAR == 14 || (VAR != 2 && VAR != 13 && !(FMT == ACT_X2F16 && SL));
 #define TVR_PP_CLUSTER(...)                  \
   __builtin_amdgcn_s_barrier();              \
   __builtin_amdgcn_sched_barrier(0);         \
-  if (VAR != 2) __builtin_amdgcn_s_setprio(1); \
+  if (prio) __builtin_amdgcn_s_setprio(1);   \
   __VA_ARGS__;                               \
-  if (VAR != 2) __builtin_amdgcn_s_setprio(0); \
+  if (prio) __builtin_amdgcn_s_setprio(0);   \
   __builtin_amdgcn_sched_barrier(0);         \
   __builtin_amdgcn_s_barrier();              \
   __builtin_amdgcn_sched_barrier(0)
@@ -516,6 +521,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  if (VAR == 13 && wr == 1) __builtin_amdgcn_s_setprio(1);  // VAR 13: static priority for the younger half
   unsigned long long d_loop0 = 0, d_loop1 = 0;
   if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
   auto kloop = [&](auto part) {
@@ -611,7 +617,8 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
-// (stale LDS: timing only), 2 no s_setprio, 3 no group offset, 4 no vmcnt
+// (stale LDS: timing only), 2 no s_setprio, 13 s_setprio 1 once for waves 4-7, 14 the cluster flips in the
+// sliced form too, 3 no group offset, 4 no vmcnt
 // waits in the loop (racy: timing only), 6 per-block stamps (start, loop
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores

@@ -140,14 +140,22 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12") {  // diagnostic variants
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12" || path == "x2pp13") {  // diagnostic variants
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
                     : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
                     : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
                     : path == "x2pp12" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 12>
+                    : path == "x2pp13" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 13>
                                       : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
           hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2ppsl" || path == "x2ppsl14" || path == "x2ppsl13") {  // sliced accumulation (6.9B / 12B)
+          grid = gemm_pingpong_grid(s.M, s.N);
+          auto ks = path == "x2ppsl" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true>
+                    : path == "x2ppsl14" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 14, false, true>
+                                        : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 13, false, true>;
+          hipLaunchKernelGGL(ks, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2ppg" || path == "x2ppg7") {  // pingpong with the QKV+MLP-in epilogue, timed
           grid = gemm_pingpong_grid(s.M, s.N);
