@@ -521,7 +521,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  if (VAR == 13 && wr == 1) __builtin_amdgcn_s_setprio(1);  // VAR 13: static priority for the younger half
+  if (VAR == 13 && wave_s >= 4) __builtin_amdgcn_s_setprio(1);  // VAR 13: static priority for the younger half (wave-uniform test)
   unsigned long long d_loop0 = 0, d_loop1 = 0;
   if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
   auto kloop = [&](auto part) {
