@@ -96,10 +96,14 @@ constexpr bool PP_NT_STORES = TVR_PP_NT;
 #define TVR_PP_SLICE_MIN_K 16384
 #endif
 constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
-// Placement of the sliced form's adds: 1 (round 5) scalar adds spread over the next pair's MFMA gaps with
-// the last pair carried into the next phase; 0 (round 4) the pair's packed adds after the next pair's MFMAs.
+// Placement of the sliced form's adds: 2 (round 5) scalar adds, two in each of the next pair's last four MFMA
+// gaps, the last pair carried into the next phase (+2.2 % on the probe's sliced shapes, C5 1,286 -> 1,317
+// patched/s, profiles/r05/slice_form2_ab_r05n.txt: form 1 spread them 2, 2, 1, 1, 1, 1 and its first adds
+// read results too soon after their MFMA, which the compiler paid for with an s_nop 3 three times per
+// cluster); 1 that form; 0 (round 4) the pair's packed adds after the next pair's MFMAs.  Same adds in the
+// same order in every form: bit-identical results.
 #ifndef TVR_PP_SLICE_FORM
-#define TVR_PP_SLICE_FORM 1
+#define TVR_PP_SLICE_FORM 2
 #endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
@@ -407,7 +411,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part, int ci, int cj) {
     if constexpr (FMT == ACT_X2F16 && SL && !decltype(part)::value) {
-#if TVR_PP_SLICE_FORM == 1
+#if TVR_PP_SLICE_FORM >= 1
       // tile pairs (i, 0..1) in turn — the pair's first products, second, third (two independent chains back
       // to back) — and the previous pair's 8 slice-sum adds (the carried pair's for i = 0) spread 2, 2, 1, 1,
       // 1, 1 over its six MFMA gaps as SCALAR v_add_f32 (the engine builds with -fno-slp-vectorize: packed
@@ -425,13 +429,20 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
                                                              p == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : t[i][j], 0, 0, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           // adds after MFMA q: elements e0 .. e1 of the previous pair's 8 (tile e / 4, element e % 4)
+#if TVR_PP_SLICE_FORM == 2
+          // form 2: none after q0 / q1, two after q2 .. q5, so that every add reads a result >= 9 issue slots after
+          // the MFMA that wrote it (form 1's adds after q0 read the previous pair's tile-0 sum 5 slots after its
+          // last MFMA: the compiler pads each with s_nop 3, 3 per cluster)
+          const int e0 = q < 2 ? 0 : 2 * (q - 2), e1 = q < 2 ? 0 : 2 * (q - 2) + 2;
+#else
           const int e0 = q < 2 ? 2 * q : q + 2, e1 = q < 2 ? 2 * q + 2 : q + 3;
+#endif
 #pragma unroll
           for (int e = e0; e < e1; ++e)
             acc[di][dj + (e >> 2)][e & 3] += i == 0 ? tc[e >> 2][e & 3] : t[i - 1][e >> 2][e & 3];
-          if (q < 2)
+          if (e1 - e0 == 2)
             __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-          else
+          else if (e1 - e0 == 1)
             __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
         }
       }
@@ -550,7 +561,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   };
   if (vi == 8) {
     kloop(std::integral_constant<bool, false>{});
-#if TVR_PP_SLICE_FORM == 1
+#if TVR_PP_SLICE_FORM >= 1
     if constexpr (FMT == ACT_X2F16 && SL) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
       acc[7][0] = slice_add(acc[7][0], tc[0]);
       acc[7][1] = slice_add(acc[7][1], tc[1]);

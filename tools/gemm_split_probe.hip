@@ -1,7 +1,8 @@
 // gemm_split_probe.hip — speed, in-kernel clock and accuracy of the three GEMM
 // paths (fp32 MFMA, 3-plane bf16 split, 2-plane fp16 split) at the engine's
 // real shapes, each checked against an fp64 reference on sampled rows.
-//   hipcc --offload-arch=gfx950 -O3 -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
+//   hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -I include -o tools/gemm_split_probe tools/gemm_split_probe.hip
+//   (-fno-slp-vectorize as the engine builds: the sliced form's adds stay scalar)
 //   tools/gemm_split_probe [f32|x3|x2|x2p|x2pg|x2pt|bf16 ...]   (default: f32 x3 x2 x2p)
 //     x2p  = the engine's planar kernel (A pre-split, LDS-DMA, 16x16x32, EPI_BIAS)
 //     x2pg = the same with the QKV+MLP-in epilogue (bias, GELU, split-plane stores)
