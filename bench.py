@@ -7,7 +7,15 @@ One step = one full CIE sweep of ``--prompts`` label-shuffled 4-shot prompts
 prompts plus 12 x 1024 patched forwards, each evaluated to the probability of
 the prompt's first answer token (scratch2.py:171-197), i.e. 12,288 units per
 GPU per step.  Weights are seeded synthetic Pythia-2.8B (no checkpoints
-offline), fp32 like the reference (TransformerLens default dtype).
+offline), fp16-valued as the released checkpoints store them (``--weights
+fp16``, default; ``fp32`` draws fp32-valued ones as rounds 1-5 did) and
+computed on in fp32 like the reference (TransformerLens loads the float16
+checkpoint into its default fp32 dtype).  With fp16-valued weights the engine
+binds the checkpoint's own GEMM weights (include/tvr.h tvr_model_set_exact16):
+their residual plane is zero, so the x2f16 GEMMs run 2 products instead of 3
+(``roofline.peak`` is then the 2-product ceiling), and a
+``processed_weights_leg`` re-times the sweep on the TL-processed weights
+(3 products) for comparison.
 
 GEMMs (95 % of the step) run on the fp32-accurate two-plane fp16 split
 (``--gemm x2f16``, default: every fp32 operand split into 2 power-of-two-scaled
@@ -114,6 +122,8 @@ def parse():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="N=1 only, planning aid: time rank 0's share of a strong-split run (--shard sites / heads) "
                          "on this many GPUs on this one GPU; value = the units of that share / its time")
+    ap.add_argument("--weights", default="fp16", choices=("fp16", "fp32"),
+                    help="synthetic weight values: fp16-valued as the released checkpoints (default) or fp32")
     ap.add_argument("--gemm", default="x2f16", choices=("x2f16", "x3bf16", "f32", "bf16"),
                     help="matrix-core path of the GEMMs (x2f16 / x3bf16 / f32 fp32-accurate; bf16 is the "
                          "north star's bf16 configuration, not the fp32 headline)")
@@ -324,8 +334,10 @@ def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
     from tvr_amd.distributed import balanced_site_shard
     from tvr_amd.experiments import causal_indirect_effect_sums
     t0 = time.time()
-    model = tvr_amd.Model.from_pretrained("pythia-12b", device=dev, seed=0, gemm=args.gemm)
+    model = tvr_amd.Model.from_pretrained("pythia-12b", device=dev, seed=0, gemm=args.gemm,
+                                          fp16_weights=args.weights == "fp16")
     cfg = model.cfg
+    x16 = bool(model.exact16)
     g = torch.Generator(device=dev).manual_seed(4321)
     mean = torch.randn(cfg.n_layers, cfg.n_heads, cfg.d_model, device=dev, generator=g) * 0.5
     prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, 10, seed=1234)
@@ -361,7 +373,7 @@ def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
             "units_per_step": units, "steps": steps, "ms_per_step": round(sec * 1e3, 1),
             "value": round(rate, 2), "unit": "patched prompts/s", "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak_all, 4),
-            "model_build_s": round(build_s, 1)}
+            "exact16_gemms": x16, "model_build_s": round(build_s, 1)}
 
 
 def rank_times(el, dev):
@@ -413,7 +425,8 @@ def config_c4(args, dev, n_tasks=3, world=1):
     from tvr_amd import distributed as D
     from tvr_amd import experiments as E
     t0 = time.time()
-    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device=dev, seed=0, gemm="bf16")
+    model = tvr_amd.Model.from_pretrained("pythia-6.9b", device=dev, seed=0, gemm="bf16",
+                                          fp16_weights=args.weights == "fp16")
     build_s = time.time() - t0
     arrow = tvr_amd.tasks.ARROW
     cie_in = {}
@@ -523,7 +536,8 @@ def cpu_baseline(args, cfg, prompts, answers, mean, model):
     # the engine's weights: the same seeded generator on the same device (synth_engine_weights),
     # processed there by the oracle's own TransformerLens restatement, then moved to the CPU
     shapes = tvr_amd.weights.hf_param_shapes(cfg)
-    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, model.device) for n, s in shapes.items()}
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, model.device, fp16=args.weights == "fp16")
+          for n, s in shapes.items()}
     oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
                                              cfg.rotary_dim, cfg.n_ctx), sd, tokenizer=None)
     del sd
@@ -586,7 +600,8 @@ def parity_informative(args, dev, cores):
     t0 = time.time()
     cfg = tvr_amd.get_config(args.model).with_(n_layers=4)
     shapes = tvr_amd.weights.hf_param_shapes(cfg)
-    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, dev, 0.05) for n, s in shapes.items()}
+    sd = {n: tvr_amd.weights.synth_param(cfg, n, s, 0, dev, 0.05, fp16=args.weights == "fp16")
+          for n, s in shapes.items()}
     model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device=dev, gemm=args.gemm)
     oracle = HookedPythiaOracle(OracleConfig(cfg.n_layers, cfg.d_model, cfg.n_heads, cfg.d_mlp, cfg.d_vocab,
                                              cfg.rotary_dim, cfg.n_ctx), sd, tokenizer=model.tokenizer)
@@ -624,6 +639,8 @@ def parity_informative(args, dev, cores):
     return out
 
 
+DTYPE_X16 = ("f32 (x2f16 emulation: fp32 activations as 2 fp16 planes against the checkpoint's exact fp16 weights, "
+             "2 MFMA products, fp32 accumulate)")
 DTYPES = {"x2f16": "f32 (x2f16 emulation: fp32 operands as 2 fp16 planes, 3 MFMA products, fp32 accumulate)",
           "x3bf16": "f32 (x3bf16 emulation: fp32 operands as 3 bf16 planes, 6 MFMA products, fp32 accumulate)",
           "f32": "f32 (v_mfma_f32_32x32x2_f32)",
@@ -656,9 +673,11 @@ def main():
 
     cfg = tvr_amd.get_config(args.model)
     t0 = time.time()
-    model = tvr_amd.Model.from_pretrained(args.model, device=dev, seed=0, gemm=args.gemm)
+    model = tvr_amd.Model.from_pretrained(args.model, device=dev, seed=0, gemm=args.gemm,
+                                          fp16_weights=args.weights == "fp16")
     torch.cuda.synchronize()
-    log(f"[rank {rank}] {args.model} synthetic weights on {dev} in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] {args.model} synthetic {args.weights}-valued weights on {dev} in {time.time() - t0:.1f}s "
+        f"(exact-fp16 GEMMs: {model.exact16})")
 
     # --- mean head activations [L, H, d]: a real extraction (a1) or seeded random
     te, n_ex, hbm_ex = None, 0, None
@@ -754,7 +773,8 @@ def main():
                                           shard, emulate, len(sites))
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    peak = PEAKS[args.gemm]
+    products = 2 if (args.gemm == "x2f16" and model.exact16) else PRODUCTS.get(args.gemm)
+    peak = BF16_MFMA_PEAK_TFLOPS / products if products else PEAKS[args.gemm]
     L, d, V = cfg.n_layers, cfg.d_model, cfg.d_vocab
     P_l = 4 * d * d + 2 * d * cfg.d_mlp
     # F_alg(site at layer l) = (L-1-l)(2 P_l T + 2 T(T+1) d) + 2 d V
@@ -783,8 +803,10 @@ def main():
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": DTYPES[args.gemm],
-        "data": f"synthetic (seeded {args.model}-shaped weights, seeded single-token shuffled-label prompts)",
+        "dtype": DTYPE_X16 if (args.gemm == "x2f16" and model.exact16) else DTYPES[args.gemm],
+        "data": f"synthetic (seeded {args.model}-shaped weights, "
+                f"{'fp16-valued as the released checkpoints' if args.weights == 'fp16' else 'fp32-valued'}; "
+                f"seeded single-token shuffled-label prompts)",
         "config": {
             "workload": workload,
             "sites_per_step": units_total,
@@ -803,7 +825,7 @@ def main():
             "frac": round(achieved / peak, 4),
             "flops_basis": "algorithmic fp32 2*M*N*K per launch / HIP-event launch time (separate profiled pass)",
             "peak_basis": ("fp32 MFMA dense peak" if args.gemm == "f32" else
-                           f"fp16/bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {PRODUCTS[args.gemm]} products "
+                           f"fp16/bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS} / {products} products "
                            f"(= fp32-equivalent ceiling of the split; fp32 MFMA peak {FP32_MFMA_PEAK_TFLOPS})"),
             "traffic": traffic,
             "traffic_source": traffic_src,
@@ -830,6 +852,19 @@ def main():
         },
     }
     out["config"]["gemm"] = args.gemm
+    out["config"]["weights"] = args.weights
+    out["config"]["exact16_gemms"] = bool(model.exact16)
+    if world == 1 and model.exact16 and not emulate:
+        # the same sweep on the TL-processed weights (3 products: the path of fp32-valued checkpoints)
+        model.set_exact16(False)
+        npw = max(1, min(args.steps, 2))
+        el_pw, cie_pw = timed(1, npw, False)
+        model.set_exact16(True)
+        out["processed_weights_leg"] = {
+            "gemm": "x2f16, 3 products on the processed (folded / centred) weights", "steps": npw,
+            "value": round(units_rank * npw / el_pw, 2),
+            "max_abs_cie_diff_vs_exact16": float((cie - cie_pw).abs().max()),
+            "max_abs_cie": float(cie_pw.abs().max())}
     if world == 1 and args.f32_leg and args.gemm != "f32":
         model.set_gemm("f32")
         n32 = max(1, min(args.steps, 2))

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define TVR_ABI_VERSION 10
+#define TVR_ABI_VERSION 11
 
 enum tvr_status {
   TVR_OK = 0,
@@ -152,6 +152,30 @@ int32_t tvr_model_get_gemm(const tvr_model* model);
  * an input outside its range (its results are then not fp32-accurate and must
  * be discarded).  Synchronises `stream`; clears the flag. */
 int tvr_model_range_status(tvr_model* model, void* stream);
+
+/* Exact-fp16 weights (the checkpoint dtype of every Pythia), for TVR_GEMM_X2F16.
+ * Per layer, caller-owned device arrays, kept alive by the caller:
+ *   w1  fp16 [3d + d_mlp][d]  the checkpoint's Q | K | V rows (engine order, as
+ *                             tvr_layer_weights.w1) and MLP-in rows BEFORE fold_ln
+ *   w2  fp16 [d][d + d_mlp]   W_O | W_out BEFORE center_writing_weights
+ *   g1, g2 fp32 [d]           LN1 / LN2 gamma (ln_1.w, ln_2.w)
+ * They must be the raw tensors the model's processed w1 / w2 were made from
+ * (tvr_layer_weights: fold_ln, centring and fold_value_biases applied to them).
+ * In X2F16 mode the QKV + MLP-in GEMM then reads LNPre(x) * gamma1 (Q, K, V
+ * columns) and * gamma2 (MLP-in columns) against w1 — fold_ln's centring of the
+ * read-in weights is a no-op on a centred LNPre row — and the O + MLP-out GEMM
+ * reads w2 uncentred: the residual stream then carries one constant per row,
+ * which every LayerNorm removes and tvr_trace_read's hook_resid_pre export
+ * subtracts.  Weights exact in fp16 need 2 matrix products per 32-deep slice
+ * instead of 3.  Results equal the processed-weight path's to fp32 rounding.
+ * Pass layers == NULL to detach.  Other modes ignore the binding. */
+typedef struct {
+  const uint16_t* w1;
+  const uint16_t* w2;
+  const float* g1;
+  const float* g2;
+} tvr_exact16_layer;
+int tvr_model_set_exact16(tvr_model* model, const tvr_exact16_layer* layers /*[n_layers] host, or NULL*/);
 
 /* Clean-run trace: every layer's hook_resid_pre, attn.hook_z and the K/V
  * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */

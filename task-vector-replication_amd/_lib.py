@@ -46,6 +46,10 @@ class CLayerWeights(ctypes.Structure):
                 ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p)]
 
 
+class CExact16Layer(ctypes.Structure):
+    _fields_ = [("w1", ctypes.c_void_p), ("w2", ctypes.c_void_p), ("g1", ctypes.c_void_p), ("g2", ctypes.c_void_p)]
+
+
 class CSite(ctypes.Structure):
     _fields_ = [("seq", ctypes.c_int32), ("kind", ctypes.c_int32), ("layer", ctypes.c_int32),
                 ("head", ctypes.c_int32), ("pos", ctypes.c_int32), ("src_seq", ctypes.c_int32),
@@ -71,7 +75,7 @@ class CHbmStats(ctypes.Structure):
 HBM_KINDS = ("entry", "capture", "lnpre", "attention", "row_stats", "lin_entry")
 
 # name -> (restype, argtypes); every symbol include/tvr.h declares.
-ABI_VERSION = 10  # include/tvr.h TVR_ABI_VERSION
+ABI_VERSION = 11  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
@@ -108,6 +112,7 @@ SIGNATURES = {
                                      ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]),
     "tvr_workspace_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
     "tvr_model_set_gemm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
+    "tvr_model_set_exact16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tvr_model_get_gemm": (ctypes.c_int32, [ctypes.c_void_p]),
     "tvr_split_planes": (ctypes.c_int, [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "tvr_gemm_x3bf16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,

@@ -92,8 +92,9 @@ struct MatW {
   const uint16_t* h = nullptr;
   size_t wps = 0;
   float wscale = 1.0f;
+  bool x16 = false;  // h is ONE plane holding the weights exactly (fp16 values: tvr_model_set_exact16)
   MatW rows(size_t elems) const {
-    return {f + elems, x ? x + elems : nullptr, h ? h + elems : nullptr, wps, wscale};
+    return {f ? f + elems : nullptr, x ? x + elems : nullptr, h ? h + elems : nullptr, wps, wscale, x16};
   }
 };
 
@@ -150,6 +151,16 @@ struct tvr_model {
   float* lin_c1 = nullptr;         // [L][D1]
   std::vector<float> lin_scale;    // per layer: X2F16 plane scale (1 for BF16)
   std::map<PlanKey, PpPlan> plans;  // plan_pp_cached: GEMM launch plans per shape
+  // Exact-fp16 weights (tvr_model_set_exact16; x2f16 mode only): the checkpoint's own W1 rows (Q | K | V |
+  // MLP-in, before fold_ln) and W2 (W_O | W_out, before center_writing_weights) as one caller-owned fp16
+  // plane each, and LN1 / LN2's gamma.  The QKV + MLP-in GEMM then reads LNPre(x) * gamma1 (Q, K, V
+  // columns) / * gamma2 (MLP-in columns) against the raw rows — fold_ln's centring of the read-in weights
+  // is a no-op on a centred LNPre row — and the O + MLP-out GEMM the raw W2, whose missing centring adds one
+  // constant to every element of a row's residual, which every LayerNorm (and the centred trace export)
+  // removes.  Both then run 2 MFMA products per slice instead of 3 (gemm_pingpong.hpp WX).
+  bool x16 = false;
+  std::vector<MatW> w1x, w2x;
+  std::vector<const float*> g1, g2;
 };
 
 struct tvr_trace {
@@ -167,6 +178,7 @@ struct tvr_trace {
   // tvr_forward_clean would) and writes these outputs; any other use of the
   // trace runs it on its own first (flush_pending).
   bool pending = false;
+  bool uncentred = false;  // filled on the exact-fp16 weight path: hook_resid_pre is centred on export
   std::vector<int32_t> p_targets;  // [n_seq] or empty
   float* p_prob = nullptr;
   int32_t* p_topk = nullptr;
@@ -313,6 +325,9 @@ int act_fmt(const tvr_model* m) {
   return m->gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : m->gemm_mode == TVR_GEMM_BF16 ? ACT_BF16 : ACT_F32;
 }
 
+// the exact-fp16 weight path (tvr_model_set_exact16) is on: x2f16 mode with the raw planes attached
+bool use_x16(const tvr_model* m) { return m->x16 && m->gemm_mode == TVR_GEMM_X2F16; }
+
 // gemm_pingpong_kernel over tiles [tile_base, tile_base + count) of a planar
 // launch's raster (count 0: all), VEC epilogue
 // Raster group (m-blocks walked before the next block column): 4, or 2 when
@@ -336,31 +351,36 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
   ep.tile_count = count;
   ep.group_m = pp_group_m(N);
   const dim3 g(count > 0 ? count : gemm_pingpong_grid(M, N));
-#define TVR_PP1(E, F, V, S)                                                                                       \
-  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V, 0, false, S>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,       \
+  const bool wx = a_fmt == ACT_X2F16 && W.x16;  // one exact fp16 weight plane: 2 products (launch_gemm checks)
+#define TVR_PP1(E, F, V, S, X)                                                                                    \
+  hipLaunchKernelGGL((gemm_pingpong_kernel<E, F, V, 0, false, S, X>), g, dim3(PP_THREADS), 0, st, Ah, 2 * lda,    \
                      (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, ep)
-#define TVR_PP1V(E, F, S) \
-  if (vec) { TVR_PP1(E, F, true, S); } else { TVR_PP1(E, F, false, S); }
+#define TVR_PP1V(E, F, S, X) \
+  if (vec) { TVR_PP1(E, F, true, S, X); } else { TVR_PP1(E, F, false, S, X); }
 #define TVR_PP1F(E)                                                                                \
   if (a_fmt == ACT_X2F16) {                                                                        \
-    if (sl) { TVR_PP1V(E, ACT_X2F16, true); } else { TVR_PP1V(E, ACT_X2F16, false); }             \
+    if (wx) {                                                                                      \
+      if (sl) { TVR_PP1V(E, ACT_X2F16, true, true); } else { TVR_PP1V(E, ACT_X2F16, false, true); } \
+    } else {                                                                                       \
+      if (sl) { TVR_PP1V(E, ACT_X2F16, true, false); } else { TVR_PP1V(E, ACT_X2F16, false, false); } \
+    }                                                                                              \
   } else {                                                                                         \
-    TVR_PP1V(E, ACT_BF16, false);                                                                  \
+    TVR_PP1V(E, ACT_BF16, false, false);                                                           \
   }
   if (a_fmt == ACT_F16) {  // the bf16 mode's Q / K columns: plain fp32 outputs only (launch_gemm checks)
-    TVR_PP1V(EPI_BIAS, ACT_F16, false);
+    TVR_PP1V(EPI_BIAS, ACT_F16, false, false);
     return;
   }
   switch (epi) {
     case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
     case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
-    case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked)
+    case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked; never one-plane weights)
       if (a_fmt != ACT_X2F16) {
-        TVR_PP1(EPI_STATS, ACT_BF16, true, false);
+        TVR_PP1(EPI_STATS, ACT_BF16, true, false, false);
       } else if (sl) {
-        TVR_PP1(EPI_STATS, ACT_X2F16, true, true);
+        TVR_PP1(EPI_STATS, ACT_X2F16, true, true, false);
       } else {
-        TVR_PP1(EPI_STATS, ACT_X2F16, true, false);
+        TVR_PP1(EPI_STATS, ACT_X2F16, true, false, false);
       }
       break;
     default: TVR_PP1F(EPI_RESID); break;
@@ -388,7 +408,16 @@ int launch_pp_splitk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(count * ksplit), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
+  pe.a2 = ep.a2;  // the exact-fp16 QKV + MLP-in launch's second A operand (by column)
+  pe.a2_col = ep.a2_col;
+  const bool wx = a_fmt == ACT_X2F16 && W.x16;
+  if (a_fmt == ACT_X2F16 && wx && sl)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true, true>), g, dim3(PP_THREADS), 0,
+                       st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16 && wx)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, false, true>), g, dim3(PP_THREADS), 0,
+                       st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true>), g, dim3(PP_THREADS), 0, st,
                        Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_X2F16)
@@ -434,7 +463,16 @@ int launch_pp_sk(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W,
   pe.tile_base = tile_base;
   pe.tile_count = count;
   const dim3 g(G), rg((unsigned)std::min<long>(4096, ((long)count * (PP_TILE_ELEMS / 4) + 255) / 256));
-  if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
+  pe.a2 = ep.a2;
+  pe.a2_col = ep.a2_col;
+  const bool wx = a_fmt == ACT_X2F16 && W.x16;
+  if (a_fmt == ACT_X2F16 && wx && sl)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true, true, true>), g, dim3(PP_THREADS), 0, st,
+                       Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16 && wx)
+    hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true, false, true>), g, dim3(PP_THREADS), 0,
+                       st, Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
+  else if (a_fmt == ACT_X2F16 && sl)  // sliced accumulation (gemm_pingpong.hpp)
     hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, true, true>), g, dim3(PP_THREADS), 0, st,
                        Ah, 2 * lda, (size_t)lda, W.h, ldw, W.wps, acc_scale, M, N, K, pe);
   else if (a_fmt == ACT_X2F16)
@@ -637,6 +675,10 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
                                  "statistics buffer");
   if (a_fmt == ACT_F16 && epi != EPI_BIAS)
     return fail(TVR_ERR_INVALID, "gemm: the fp16 operand format has the plain (bias) epilogue only");
+  if (W.x16 && (a_fmt != ACT_X2F16 || epi == EPI_STATS))
+    return fail(TVR_ERR_INVALID, "gemm: one-plane exact fp16 weights take x2f16 activations and no statistics epilogue");
+  if (ep.a2 && (a_fmt == ACT_F32 || ep.a2_col % 256 != 0))
+    return fail(TVR_ERR_INVALID, "gemm: a second A operand needs a planar format and a 256-column boundary");
   if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0) ||
       ((a_fmt == ACT_BF16 || a_fmt == ACT_F16) && K % 64 != 0))
     return fail(TVR_ERR_UNSUPPORTED, "gemm: K, lda, ldw must be multiples of 32/4/4 (8 for planes, K of 64 for "
@@ -656,7 +698,7 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     // PP_SLICE_MIN_K (6.9B, 12B), or on any launch of that K
     const bool sl = a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (m && m->K2 >= PP_SLICE_MIN_K));
     if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec &&
-        a_fmt != ACT_F16) {
+        a_fmt != ACT_F16 && !W.x16 && !ep.a2) {
       // a few rows (the linearised entry's G on a rank of a head split): gemm_skinny.hpp
       const dim3 g(gemm_skinny_grid(N));
 #define TVR_SK(F, MT)                                                                                  \
@@ -877,27 +919,33 @@ int ensure_lin(tvr_model* m, hipStream_t st) {
 // y: fp32 [rows][ldy] (ACT_F32) or a planar activation format
 // copy: rows < copy_rows of x also go there unchanged (same stride; a fused
 // sweep's clean rows into the trace's hook_resid_pre)
+// g1 / g2 / y2 (x2f16, exact-fp16 weights): y = LNPre(x) * g1 and y2 = LNPre(x) * g2 (range-checked)
 int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, int rows,
                  int d, float eps, int fmt, hipStream_t st, tvr_model* m = nullptr, float2* stats = nullptr,
-                 float* copy = nullptr, int copy_rows = 0) {
+                 float* copy = nullptr, int copy_rows = 0, const float* g1 = nullptr, const float* g2 = nullptr,
+                 void* y2 = nullptr) {
   if (rows <= 0) return TVR_OK;
   ProfSpan ps(m, st);
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
     return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
+  if (g1 && (fmt != ACT_X2F16 || !g2 || !y2 || !m))
+    return fail(TVR_ERR_INTERNAL, "lnpre: the gamma-scaled pair is an x2f16 model path");
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
   if (fmt == ACT_X2F16)
     hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows);
+                       copy_rows, g1, g2, y2, m ? m->range_flag : nullptr);
   else if (fmt == ACT_BF16)
     hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows);
+                       copy_rows, nullptr, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows);
+                       copy_rows, nullptr, nullptr, nullptr, nullptr);
   TVR_HIP(hipGetLastError());
-  // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element)
-  ps.done(TVR_HBM_LNPRE, (double)rows * d * 8.0 + (copy ? (double)std::min(rows, copy_rows) * d * 4.0 : 0.0));
+  // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element;
+  // the gamma-scaled pair two x2f16 rows)
+  ps.done(TVR_HBM_LNPRE, (double)rows * d * (g1 ? 12.0 : 8.0) +
+                             (copy ? (double)std::min(rows, copy_rows) * d * 4.0 : 0.0));
   return TVR_OK;
 }
 
@@ -909,6 +957,8 @@ struct Acts {
   float* qkv;     // [R][3d]
   float* a2;      // [R][K2]  (z | gelu(mlp-in))
   int fmt;
+  // exact-fp16 weights (use_x16): xn holds LNPre(resid) * gamma1 and xn2 [R][d] LNPre(resid) * gamma2
+  float* xn2 = nullptr;
   // a fused clean + patch sweep: rows < mirror_rows (the clean rows) of the
   // layer's resid_pre (LayerNorm's input) and qkv (the QKV epilogue's fp32
   // columns) are also written to the trace by the kernels producing them
@@ -1040,10 +1090,41 @@ double attention_bytes(int d, int q_rows, int kv_rows, int fmt, int zf_rows) {
 // EPI_SPLIT_GELU fp32).  TVR_GEMM_BF16 runs the attention-score columns
 // (Q, K: [0, 2d)) on the fp16 operands instead (W1's fp16 Q / K plane, xn's
 // fp16 plane 1: store_ln4) with plain fp32 stores, the rest on bf16.
-int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const GemmEpi& ep, hipStream_t st) {
+// xn2 (use_x16): xn / xn2 are LNPre rows scaled by gamma1 / gamma2, and the GEMM runs on the raw W1 rows
+// (one exact fp16 plane): the Q | K | V columns [0, 3d) read xn, the MLP-in columns xn2 — per tile in one
+// launch when the boundary falls on a 256-column tile edge of the launch, else as two launches.
+int launch_w1(tvr_model* m, int l, const void* xn, int M, int c0, int N, const GemmEpi& ep, hipStream_t st,
+              const void* xn2 = nullptr) {
   const int d = m->cfg.d_model;
   const int fmt = act_fmt(m);
   const int epi = fmt != ACT_F32 ? EPI_SPLIT_GELU_ACT : EPI_SPLIT_GELU;
+  if (xn2) {
+    if (!use_x16(m) || fmt != ACT_X2F16) return fail(TVR_ERR_INTERNAL, "launch_w1: gamma-scaled rows off the x16 path");
+    const MatW W = m->w1x[l].rows((size_t)c0 * d);
+    const int qkv_end = 3 * d - c0;  // first column of the launch that reads xn2
+    if (qkv_end <= 0)
+      return launch_gemm(epi, xn2, d, fmt, W, d, M, N, d, ep, st, m);
+    if (qkv_end >= N)
+      return launch_gemm(epi, xn, d, fmt, W, d, M, N, d, ep, st, m);
+    if (qkv_end % 256 == 0) {
+      GemmEpi e = ep;
+      e.a2 = static_cast<const uint16_t*>(xn2);
+      e.a2_col = qkv_end;
+      return launch_gemm(epi, xn, d, fmt, W, d, M, N, d, e, st, m);
+    }
+    // two launches: columns [c0, 3d) below the GELU split, then the MLP-in columns (their GELU outputs and raw
+    // pre-activations are indexed from n_split, which becomes 0)
+    GemmEpi e1 = ep;
+    e1.n_split = std::min(ep.n_split, qkv_end);
+    TVR_TRY(launch_gemm(epi, xn, d, fmt, W, d, M, qkv_end, d, e1, st, m));
+    GemmEpi e2 = ep;
+    e2.bias = ep.bias ? ep.bias + qkv_end : nullptr;
+    e2.out0 = ep.out0 ? ep.out0 + qkv_end : nullptr;
+    if (ep.out0m) e2.out0m = ep.out0m + qkv_end;
+    e2.n_split = ep.n_split - qkv_end;
+    if (e2.n_split < 0) return fail(TVR_ERR_INTERNAL, "launch_w1: MLP-in columns below the GELU split");
+    return launch_gemm(epi, xn2, d, fmt, W.rows((size_t)qkv_end * d), d, M, N - qkv_end, d, e2, st, m);
+  }
   const int nqk = fmt == ACT_BF16 && !m->w1qk.empty() ? std::min(std::max(2 * d - c0, 0), N) : 0;
   if (nqk > 0) {
     GemmEpi e{};
@@ -1076,9 +1157,9 @@ int run_block(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n_seqs, int
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
   TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m, nullptr, a.resid_mirror,
-                       a.mirror_rows));
+                       a.mirror_rows, a.xn2 ? m->g1[l] : nullptr, a.xn2 ? m->g2[l] : nullptr, a.xn2));
   const GemmEpi e1 = epi_qkv_mlpin(m, w.b1, qkv_out, a);
-  TVR_TRY(launch_w1(m, l, a.xn, R, 0, m->D1, e1, st));
+  TVR_TRY(launch_w1(m, l, a.xn, R, 0, m->D1, e1, st, a.xn2));
   ProfSpan ps(m, st);
   TVR_TRY(launch_attention(m, qkv_out, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows,
                            row_from));
@@ -1102,17 +1183,17 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   const int d = c.d_model;
   const tvr_layer_weights& w = m->layers[l];
   TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, R, d, c.ln_eps, a.fmt, st, m, nullptr, a.resid_mirror,
-                       a.mirror_rows));
+                       a.mirror_rows, a.xn2 ? m->g1[l] : nullptr, a.xn2 ? m->g2[l] : nullptr, a.xn2));
   GemmEpi kv{};  // K | V columns (w1 rows [d, 3d)) for every row (all below n_split: no GELU)
   kv.bias = w.b1 + d;
   kv.out0 = a.qkv + d;
   kv.ld0 = 3 * d;
   kv.n_split = 2 * d;
-  TVR_TRY(launch_w1(m, l, a.xn, R, d, 2 * d, kv, st));
+  TVR_TRY(launch_w1(m, l, a.xn, R, d, 2 * d, kv, st, a.xn2));
   GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);  // all columns for the last rows, gathered and scattered in place
   e1.a_rows = d_last;
   e1.out_rows = d_last;
-  TVR_TRY(launch_w1(m, l, a.xn, n_last, 0, m->D1, e1, st));
+  TVR_TRY(launch_w1(m, l, a.xn, n_last, 0, m->D1, e1, st, a.xn2));
   ProfSpan ps(m, st);
   TVR_TRY(launch_attention(m, a.qkv, cache_qkv, d_seqs, n_seqs, maxT, a.a2, a.fmt, zf, st, zf_last, zf_rows,
                            row_from));
@@ -1126,7 +1207,8 @@ int run_block_last_rows(tvr_model* m, int l, int R, const SeqDesc* d_seqs, int n
   e2.ldr = d;
   e2.a_rows = d_last;
   e2.out_rows = d_last;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, m->w2[l], m->K2, n_last, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, use_x16(m) ? m->w2x[l] : m->w2[l], m->K2, n_last, d, m->K2, e2,
+                     st, m);
 }
 
 int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
@@ -1138,7 +1220,7 @@ int run_block_out(tvr_model* m, int l, int R, Acts& a, hipStream_t st) {
   e2.ld0 = d;
   e2.resid = a.resid;
   e2.ldr = d;
-  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, m->w2[l], m->K2, R, d, m->K2, e2, st, m);
+  return launch_gemm(EPI_RESID, a.a2, m->K2, a.fmt, use_x16(m) ? m->w2x[l] : m->w2[l], m->K2, R, d, m->K2, e2, st, m);
 }
 
 // Final LN + unembed of selected rows + softmax target prob + top-k, chunked.
@@ -1321,6 +1403,49 @@ size_t tvr_workspace_bytes(const tvr_model* m) { return m ? m->ws_bytes : 0; }
 
 int32_t tvr_model_get_gemm(const tvr_model* m) { return m ? m->gemm_mode : -1; }
 
+// X2F16 mode: the weight planes again for the current exact-fp16 binding (with / without the w2 planes),
+// on the null stream
+static int replan_x2f16(tvr_model* m) {
+  if (m->gemm_mode != TVR_GEMM_X2F16) return TVR_OK;
+  TVR_TRY(tvr_model_set_gemm(m, TVR_GEMM_F32, nullptr));
+  return tvr_model_set_gemm(m, TVR_GEMM_X2F16, nullptr);
+}
+
+int tvr_model_set_exact16(tvr_model* m, const tvr_exact16_layer* layers) {
+  if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_exact16: null model");
+  const tvr_config& c = m->cfg;
+  if (!layers) {
+    const bool was = m->x16;
+    m->x16 = false;
+    m->w1x.clear();
+    m->w2x.clear();
+    m->g1.clear();
+    m->g2.clear();
+    return was ? replan_x2f16(m) : TVR_OK;
+  }
+  for (int l = 0; l < c.n_layers; ++l)
+    if (!layers[l].w1 || !layers[l].w2 || !layers[l].g1 || !layers[l].g2)
+      return fail(TVR_ERR_INVALID, "tvr_model_set_exact16: null array in layer " + std::to_string(l));
+  // the one-plane kernel's staging reads rows of 8-halve chunks and d of 4-float groups (launch_gemm's K / ld
+  // checks cover the rest)
+  if (c.d_model % 32 != 0 || m->K2 % 32 != 0)
+    return fail(TVR_ERR_UNSUPPORTED, "tvr_model_set_exact16: d_model and d_model + d_mlp must be multiples of 32");
+  m->w1x.clear();
+  m->w2x.clear();
+  m->g1.clear();
+  m->g2.clear();
+  for (int l = 0; l < c.n_layers; ++l) {
+    // one plane of the raw values themselves: weight scale 1 (fp16 subnormals reach the matrix cores as
+    // they are: tools/denorm_probe.py), no second plane (wps 0 is never read: WX kernels only)
+    m->w1x.push_back(MatW{nullptr, nullptr, layers[l].w1, 0, 1.0f, true});
+    m->w2x.push_back(MatW{nullptr, nullptr, layers[l].w2, 0, 1.0f, true});
+    m->g1.push_back(layers[l].g1);
+    m->g2.push_back(layers[l].g2);
+  }
+  m->x16 = true;
+  return replan_x2f16(m);
+}
+
 int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_gemm: null model");
   if (mode != TVR_GEMM_F32 && mode != TVR_GEMM_X3BF16 && mode != TVR_GEMM_X2F16 && mode != TVR_GEMM_BF16)
@@ -1352,19 +1477,26 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   const size_t nu = (size_t)c.d_vocab * c.d_model;
   const int np = mode == TVR_GEMM_X3BF16 ? 3 : mode == TVR_GEMM_X2F16 ? 2 : 1;
   const size_t nqk = (size_t)2 * c.d_model * c.d_model;  // BF16: W1's Q / K rows as an fp16 plane
-  const size_t total = np * ((n1 + n2) * L + nu) + (mode == TVR_GEMM_BF16 ? nqk * L : 0);
+  const size_t total = np * ((n1 + (mode == TVR_GEMM_X2F16 && m->x16 ? 0 : n2)) * L + nu) +
+                       (mode == TVR_GEMM_BF16 ? nqk * L : 0);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
     (void)hipGetLastError();
     return fail(TVR_ERR_NOMEM, "tvr_model_set_gemm: weight planes (" + std::to_string(total * 2) +
                                    " bytes) do not fit");
   }
-  // every GEMM weight matrix in order: w1[0], w2[0], ..., w1[L-1], w2[L-1], wu
+  // every GEMM weight matrix in order: w1[0], w2[0], ..., w1[L-1], w2[L-1], wu — in X2F16 with exact-fp16
+  // weights bound (tvr_model_set_exact16) without the w2 planes: the O + MLP-out GEMM reads the raw w2
+  // (12B: 19 GB not allocated); w1's planes stay (the linearised entry's G reads the processed rows)
+  const bool skip_w2 = mode == TVR_GEMM_X2F16 && m->x16;
   std::vector<MatW*> mats;
   std::vector<size_t> sizes;
   for (int l = 0; l < L; ++l) {
     mats.push_back(&m->w1[l]); sizes.push_back(n1);
-    mats.push_back(&m->w2[l]); sizes.push_back(n2);
+    if (!skip_w2) {
+      mats.push_back(&m->w2[l]);
+      sizes.push_back(n2);
+    }
   }
   mats.push_back(&m->wu); sizes.push_back(nu);
   if (mode == TVR_GEMM_BF16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
@@ -1567,6 +1699,14 @@ int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, 
   if (what == TVR_TRACE_RESID_PRE && layer >= 0 && layer <= L) src = t->resid + layer * stride;
   if (what == TVR_TRACE_Z && layer >= 0 && layer < L) src = t->z + layer * stride;
   if (!src) return fail(TVR_ERR_INVALID, "tvr_trace_read: bad hook/layer");
+  if (what == TVR_TRACE_RESID_PRE && t->uncentred && t->n_tokens > 0) {
+    // TL's residual stream is centred (every write to it is: W_E, W_O, W_out, their biases); the x16 path's
+    // differs from it by one constant per row
+    hipLaunchKernelGGL(center_rows_kernel, dim3((t->n_tokens + 3) / 4), dim3(256), 0, (hipStream_t)stream, src, dst,
+                       t->n_tokens, d);
+    TVR_HIP(hipGetLastError());
+    return TVR_OK;
+  }
   TVR_HIP(hipMemcpyAsync(dst, src, (size_t)t->n_tokens * d * sizeof(float), hipMemcpyDeviceToDevice,
                          (hipStream_t)stream));
   return TVR_OK;
@@ -1613,6 +1753,7 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
       return fail(TVR_ERR_INVALID, "token id " + std::to_string(tokens[r]) + " out of range");
   if (trace && (n_seq > trace->max_seqs || R > trace->max_tokens))
     return fail(TVR_ERR_INVALID, "trace capacity exceeded");
+  if (trace) trace->uncentred = use_x16(m);
 
   std::vector<SeqDesc> seqs(n_seq);
   for (int s = 0; s < n_seq; ++s) seqs[s] = {off[s], seq_lens[s], 0, -1, 0, 0};
@@ -1672,6 +1813,7 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
   const size_t o_tg = cv.take<int32_t>(n_seq);
   const size_t o_resid = cv.take<float>((size_t)R * d);
   const size_t o_xn = cv.take<float>((size_t)R * d);
+  const size_t o_xn2 = use_x16(m) ? cv.take<float>((size_t)R * d) : 0;
   const size_t o_qkv = trace ? 0 : cv.take<float>((size_t)R * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)R * m->K2);
   const size_t o_xf = cv.take<float>((size_t)FC * d);
@@ -1697,6 +1839,7 @@ int forward_impl(tvr_model* m, tvr_trace* trace, const int32_t* tokens, const fl
   const int fmt = act_fmt(m);
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), trace ? nullptr : (float*)(base + o_qkv),
          (float*)(base + o_a2), fmt};
+  if (use_x16(m)) a.xn2 = (float*)(base + o_xn2);
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const int32_t* d_last = (const int32_t*)(base + o_last);
   const size_t tstride = trace ? (size_t)trace->max_tokens * d : 0;
@@ -1844,6 +1987,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   // buffer, and the trace is filled as the layers go.  This removes the clean
   // forward's own small-M launches (52 prompts x 3 tokens).
   const bool fused = trace->pending;
+  if (fused) trace->uncentred = use_x16(m);  // this sweep fills the trace's clean rows
   const int Rc = fused ? trace->n_tokens : 0, nc = fused ? trace->n_seq : 0;
 
   // --- plan -----------------------------------------------------------------
@@ -2105,6 +2249,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const size_t o_egroups = cv.take<int2>(egroups.size());
   const size_t o_resid = cv.take<float>((size_t)RA * d);
   const size_t o_xn = cv.take<float>((size_t)RA * d);
+  const size_t o_xn2 = use_x16(m) ? cv.take<float>((size_t)RA * d) : 0;
   const size_t o_qkv = cv.take<float>((size_t)RA * 3 * d);
   const size_t o_a2 = cv.take<float>((size_t)RA * m->K2);
   const size_t o_xf = cv.take<float>((size_t)std::max(FCs, FCc) * d);
@@ -2140,6 +2285,7 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const int fmt = act_fmt(m);
   Acts a{(float*)(base + o_resid), (float*)(base + o_xn), (float*)(base + o_qkv),
          (float*)(base + o_a2), fmt};
+  if (use_x16(m)) a.xn2 = (float*)(base + o_xn2);
   const SeqDesc* d_seqs = (const SeqDesc*)(base + o_seqs);
   const EntryDesc* d_ents = (const EntryDesc*)(base + o_ents);
   const size_t tstride = (size_t)trace->max_tokens * d;
@@ -2209,12 +2355,12 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     const tvr_layer_weights& w = m->layers[l];
     const int Rp = Rc + rows_le[l - 1], D1 = m->D1;
     TVR_TRY(launch_lnpre(a.resid, d, nullptr, a.xn, d, Rl, d, c.ln_eps, fmt, st, m, lnstats, a.resid_mirror,
-                         a.mirror_rows));
+                         a.mirror_rows, a.xn2 ? m->g1[l] : nullptr, a.xn2 ? m->g2[l] : nullptr, a.xn2));
     GemmEpi e1 = epi_qkv_mlpin(m, w.b1, a.qkv, a);
     e1.raw = raw_h;
     e1.raw_rows = Rc;
     e1.ld_raw = c.d_mlp;
-    TVR_TRY(launch_w1(m, l, a.xn, Rp, 0, D1, e1, st));
+    TVR_TRY(launch_w1(m, l, a.xn, Rp, 0, D1, e1, st, a.xn2));
     ProfSpan ps(m, st);
     const bool prof = m->prof;
     m->prof = false;  // G and the entry rows are timed as one HBM-kind span, not as GEMM-family launches

@@ -112,6 +112,11 @@ struct GemmEpi {
   // K / V cache (EPI_BIAS, EPI_SPLIT_GELU, EPI_SPLIT_GELU_ACT below n_split)
   float* out0m;
   int mirror_rows;
+  // gemm_pingpong_kernel: tiles whose first column is >= a2_col stage their A rows from a2 instead of A
+  // (same row / plane strides): the exact-fp16-weight QKV + MLP-in launch, whose Q | K | V columns read
+  // LN1's gamma-scaled rows and whose MLP-in columns read LN2's (engine.hip, exact16)
+  const uint16_t* a2;
+  int a2_col;
   // EPI_BIAS planar launches of at most SK_MAX_M rows that opt in run
   // gemm_skinny.hpp (the linearised entry's G); the unembed keeps the pingpong
   // kernel so its logits path and fused statistics share one GEMM

@@ -299,7 +299,7 @@ struct PpLds {
 // tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256 tile
 // (split-K / stream-K), else the launch's fused epilogue.  (A separate int
 // flag: testing the pointer itself made hipcc spill 26-66 VGPRs.)
-template <int EPI, int FMT, bool VEC, int VAR, bool SL>
+template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX = false>
 __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda, size_t aps,
                                         const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale, int M,
                                         int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part, int has_part,
@@ -311,7 +311,11 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   constexpr int RPP = 64 / CPR;        // rows per 1 KB piece
   constexpr int PPP = 128 / RPP;       // pieces per plane per region (128 rows)
   constexpr int PL = 256 * BK;         // halves per plane per buffer
-  constexpr int BUF = PpLds<FMT>::BUF; // halves per buffer: A planes, then W planes
+  // WX (x2f16 only): the weights are exact in fp16 (their residual plane is zero), so only plane 0 is
+  // staged and read and the a0 w1 product is dropped: 2 products per 32-deep slice instead of 3
+  static_assert(!WX || FMT == ACT_X2F16, "one-plane weights: x2f16 activations only");
+  constexpr int WNPL = WX ? 1 : NPL;   // weight planes staged
+  constexpr int BUF = (NPL + WNPL) * PL; // halves per buffer: A planes, then W planes
   constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
   static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
   static_assert(PpLds<FMT>::HALVES * 2 <= 160 * 1024, "LDS budget");
@@ -333,13 +337,15 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   // (M0) are then scalar, so a stage costs one VALU address add per piece
   // instead of five (add, select, shift, readfirstlane for M0, address).
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const uint16_t* Ab = ep.a2 != nullptr && n0 >= ep.a2_col ? ep.a2 : A;  // this tile's A operand
   const uint16_t* src[4][2];
   int dst[4][2];
 #pragma unroll
   for (int R = 0; R < 4; ++R) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int pi = 2 * wave_s + s;
+      // pieces of a one-plane weight region (WX): one per wave (s = 0), plane 0
+      const int pi = (WX && R >= 2) ? wave_s : 2 * wave_s + s;
       const int plane = pi / PPP, x0 = (pi % PPP) * RPP;  // region row of the piece's first row
       int trow0;                                          // tile row of it
       if (R < 2)
@@ -350,7 +356,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       const int chunk = (lane % CPR) ^ planar_g<CPR>(row);
       if (R < 2) {
         const int am = min(m0 + row, M - 1);
-        src[R][s] = A + plane * aps + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + chunk * 8;
+        src[R][s] = Ab + plane * aps + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + chunk * 8;
         dst[R][s] = plane * PL + trow0 * BK;
       } else {
         src[R][s] = W + plane * wps + (size_t)min(n0 + row, N - 1) * ldw + chunk * 8;
@@ -364,7 +370,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     const int koff = live && VAR != 12 ? (kbeg + kt) * BK : 0;  // VAR 12: every k-tile re-reads k-tile 0 (L2-hot)
     const int boff = (kt & 1) * BUF;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
+    for (int s = 0; s < ((WX && R >= 2) ? 1 : 2); ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
   };
 
   // ---- fragment offsets (halves, within a buffer); f = plane (x2f16) or k group (bf16)
@@ -404,13 +410,13 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int f = 0; f < 2; ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
+      for (int f = 0; f < (WX ? 1 : 2); ++f) fw[j][f] = *(const frag*)(base + boff[f] + (j0 + j) * 16 * BK);
   };
   // sliced form, all 8 tiles live: the slice sums of the cluster's LAST tile pair are carried into the next
   // phase's cluster (tc, for acc[ci][cj + 0..1]) and added there, while its first MFMAs run
   [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part, int ci, int cj) {
-    if constexpr (FMT == ACT_X2F16 && SL && !decltype(part)::value) {
+    if constexpr (FMT == ACT_X2F16 && SL && !WX && !decltype(part)::value) {
 #if TVR_PP_SLICE_FORM >= 1
       // tile pairs (i, 0..1) in turn — the pair's first products, second, third (two independent chains back
       // to back) — and the previous pair's 8 slice-sum adds (the carried pair's for i = 0) spread 2, 2, 1, 1,
@@ -484,12 +490,13 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
         f32x4 c = acc[i0 + i][j0 + j];
         if constexpr (FMT == ACT_X2F16 && SL) {  // the slice's sum first, then one add (see above)
           f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t, 0, 0, 0);
+          if constexpr (!WX) t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t, 0, 0, 0);
           t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], t, 0, 0, 0);
           c = slice_add(c, t);
         } else if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
+          if constexpr (VAR != 15 && !WX)  // (VAR 15, probe timing: the product dropped on full staging)
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
         } else if constexpr (FMT == ACT_F16) {
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
@@ -524,7 +531,11 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   stage(3, 0);
   stage(0, 1);
   stage(2, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  // counted waits: the pieces issued after the awaited region (2 per wave per region; 1 for a WX weight region)
+  if constexpr (WX)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   if (wr == 1 && VAR != 3) {  // the group offset: waves 4-7 run one barrier behind
@@ -541,12 +552,20 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       // q1: Q(A_lo, W_lo)
       read_a(cur, 0, part);
       read_w(cur, 0, fwl, part);
-      if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
+      if constexpr (WX) {
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      } else {
+        if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
+      }
       stage(1, kt + 1);
       TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part, 7, 0));  // (ci, cj): the carried pair of the previous phase
       // q2: Q(A_lo, W_hi)
       read_w(cur, 2, fwh, part);
-      if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+      if constexpr (WX) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+      }
       stage(3, kt + 1);
       TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part, 3, 0));
       // q3: Q(A_hi, W_hi)
@@ -554,7 +573,11 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       stage(0, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part, 3, 2));
       // q4: Q(A_hi, W_lo)
-      if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
+      if constexpr (WX) {
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      } else {
+        if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
+      }
       stage(2, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part, 7, 2));
     }
@@ -562,7 +585,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   if (vi == 8) {
     kloop(std::integral_constant<bool, false>{});
 #if TVR_PP_SLICE_FORM >= 1
-    if constexpr (FMT == ACT_X2F16 && SL) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
+    if constexpr (FMT == ACT_X2F16 && SL && !WX) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
       acc[7][0] = slice_add(acc[7][0], tc[0]);
       acc[7][1] = slice_add(acc[7][1], tc[1]);
     }
@@ -635,8 +658,9 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
 // same instruction stream: timing only).  SKM: the stream-K form (sk_blocks
-// blocks; EPI_BIAS partial tiles only).  SL: x2f16 sliced accumulation (above).
-template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false, bool SL = false>
+// blocks; EPI_BIAS partial tiles only).  SL: x2f16 sliced accumulation (above).  WX: x2f16 activations
+// against weights exact in fp16 (one plane staged, two products; pp_tile).
+template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false, bool SL = false, bool WX = false>
 __global__ void __launch_bounds__(PP_THREADS, 1)
 gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const uint16_t* __restrict__ W, int ldw,
                      size_t wps, float acc_scale, int M, int N, int K, GemmEpi ep) {
@@ -671,7 +695,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       const int nk = (int)min((long long)(nk_all - kbeg), it1 - it);
       int m0, n0;
       pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-      pp_tile<EPI, FMT, VEC, VAR, SL>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+      pp_tile<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                   ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, 1, st0, sr0);
       it += nk;
     };
@@ -687,7 +711,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
     const int kbeg = (int)((long long)split * nk_all / S);
     const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
-    pp_tile<EPI, FMT, VEC, VAR, SL>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+    pp_tile<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                 ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS, S > 1, st0, sr0);
   }
 }

@@ -62,18 +62,42 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
   }
 }
 
+// dst[r] = src[r] - mean(src[r]) (one wave per row, d % 4 == 0): the exact-fp16 weight path's residual
+// stream carries one extra constant per row (engine.hip tvr_model, x16), which the TL residual lacks
+__global__ void center_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int d) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (r >= rows) return;
+  const float4* x = (const float4*)(src + (size_t)r * d);
+  float4* y = (float4*)(dst + (size_t)r * d);
+  float s = 0.f;
+  for (int c = lane; c < d / 4; c += 64) {
+    const float4 v = x[c];
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  const float mean = wave_sum(s) / (float)d;
+  for (int c = lane; c < d / 4; c += 64) {
+    const float4 v = x[c];
+    y[c] = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // LayerNormPre (TL, after fold_ln): x -= mean(x); x /= sqrt(mean(x^2) + eps).
 // One wave per row; rows optionally gathered through `row_idx`.  FMT: y is
 // fp32 (ACT_F32) or a planar activation format (split.hpp; ldy counts logical
 // elements); the outputs are bounded by sqrt(d), so no range check.
 constexpr int LN_REG_F4 = 20;  // float4 per lane held in registers: d <= 5120 (Pythia-12B), d % 256 == 0
+// g1 (x2f16, engine.hip's exact-fp16 weights): y = LNPre(x) * g1 and y2 = LNPre(x) * g2 instead (LN1's
+// and LN2's gamma, the read-in weights' fold_ln scale moved onto the rows), range-checked into flag.
 template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
                              void* __restrict__ y, int ldy, int rows, int d,
                              float eps, float2* __restrict__ stats, float* __restrict__ copy = nullptr,
-                             int copy_rows = 0) {
+                             int copy_rows = 0, const float* __restrict__ g1 = nullptr,
+                             const float* __restrict__ g2 = nullptr, void* __restrict__ y2 = nullptr,
+                             unsigned* __restrict__ flag = nullptr) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;
@@ -107,6 +131,27 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     }
     const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
     if (stats && lane == 0) stats[r] = make_float2(mean, scale);
+    if constexpr (FMT == ACT_X2F16) {
+      if (g1) {  // the two gamma-scaled rows
+        float mx = 0.f;
+#pragma unroll
+        for (int u = 0; u < LN_REG_F4; ++u) {
+          if (u < nv) {
+            const int c = lane + 64 * u;
+            const float4 o = make_float4(v[u].x / scale, v[u].y / scale, v[u].z / scale, v[u].w / scale);
+            const float4 a = ((const float4*)g1)[c], b = ((const float4*)g2)[c];
+            const float4 p = make_float4(o.x * a.x, o.y * a.y, o.z * a.z, o.w * a.w);
+            const float4 q = make_float4(o.x * b.x, o.y * b.y, o.z * b.z, o.w * b.w);
+            store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
+            store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
+            mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
+                                 fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w)))));
+          }
+        }
+        if (mx * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
+        return;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < LN_REG_F4; ++u) {
       if (u < nv) {
@@ -136,16 +181,30 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
   }
   const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
   if (stats && lane == 0) stats[r] = make_float2(mean, scale);
+  float mx = 0.f;
   for (int c = lane; c < d4; c += 64) {
     float4 v = xr[c];
     v.x = (v.x - mean) / scale; v.y = (v.y - mean) / scale;
     v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
+    if constexpr (FMT == ACT_X2F16) {
+      if (g1) {
+        const float4 a = ((const float4*)g1)[c], b = ((const float4*)g2)[c];
+        const float4 p = make_float4(v.x * a.x, v.y * a.y, v.z * a.z, v.w * a.w);
+        const float4 q = make_float4(v.x * b.x, v.y * b.y, v.z * b.z, v.w * b.w);
+        store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
+        store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
+        mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
+                             fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w)))));
+        continue;
+      }
+    }
     if constexpr (FMT != ACT_F32) {
       store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, v.x, v.y, v.z, v.w);
     } else {
       ((float4*)((float*)y + (size_t)r * ldy))[c] = v;
     }
   }
+  if (mx * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
 }
 
 // ---------------------------------------------------------------------------

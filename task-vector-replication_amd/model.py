@@ -156,19 +156,28 @@ class Model(TokenizerMixin):
                 "tvr_model_create")
         self._h = h
         self._trace_cache: Optional[Trace] = None
+        self.exact16 = False
+        self._x16_c = None
+        self.gemm = "f32"
+        if weights.raw16 is not None:  # bound first: the x2f16 planes are then built without W2's
+            self.set_exact16(True)
         self.set_gemm(gemm)
 
     # ------------------------------------------------------------------ build
     @classmethod
     def from_pretrained(cls, name: str, device="cuda", seed: int = 0, checkpoint: Optional[str] = None,
                         tokenizer_path: Optional[str] = None, std: float = 0.02, ln_std: float = 0.1,
-                        cfg: Optional[PythiaConfig] = None, gemm: str = DEFAULT_GEMM) -> "Model":
+                        cfg: Optional[PythiaConfig] = None, gemm: str = DEFAULT_GEMM,
+                        fp16_weights: bool = False) -> "Model":
         """``HookedTransformer.from_pretrained`` without a network: the named
         Pythia shape with seeded synthetic weights (generated on the device), or
         a local HF-layout safetensors ``checkpoint`` (file, or directory with
         model.safetensors / sharded index; its config.json, when present,
         supplies the shape for names this module does not know).  ``gemm``
-        picks the matrix-core path (see :meth:`set_gemm`)."""
+        picks the matrix-core path (see :meth:`set_gemm`).  ``fp16_weights``:
+        the synthetic parameters are fp16-valued, as the released checkpoints
+        are; with fp16-valued weights (synthetic or a checkpoint's) the
+        exact-fp16 GEMMs are bound (:meth:`set_exact16`)."""
         import os
         if cfg is None:
             try:
@@ -181,8 +190,10 @@ class Model(TokenizerMixin):
         if checkpoint:
             w = process_to_engine(cfg, load_hf_safetensors(checkpoint, cfg), device=dev, free_source=True)
         else:
-            w = synth_engine_weights(cfg, seed=seed, device=dev, std=std, ln_std=ln_std)
+            w = synth_engine_weights(cfg, seed=seed, device=dev, std=std, ln_std=ln_std, fp16=fp16_weights)
         tok = HFTokenizer(tokenizer_path) if tokenizer_path else None
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()  # the generation's temporaries: the engine's own allocations come next
         return cls(cfg, w, tokenizer=tok, device=dev, gemm=gemm)
 
     @classmethod
@@ -208,6 +219,34 @@ class Model(TokenizerMixin):
             _lib.check(self._lib.tvr_model_set_gemm(self._h, _lib.GEMM_MODES[mode], self._stream()),
                        "tvr_model_set_gemm")
         self.gemm = mode
+
+    def set_exact16(self, on: bool) -> None:
+        """Bind (or detach) the checkpoint's own fp16 GEMM weights
+        (``EngineWeights.raw16``; include/tvr.h ``tvr_model_set_exact16``): in
+        x2f16 mode the QKV + MLP-in and O + MLP-out GEMMs then run 2 matrix
+        products per slice instead of 3 on those exact operands, with LN's
+        gamma applied to the rows.  On by default whenever the weights are
+        fp16-valued (every released Pythia checkpoint).  Results equal the
+        processed-weight path's to fp32 rounding."""
+        raw = self.weights.raw16
+        if on and raw is None:
+            raise ValueError("set_exact16: the weights are not exact in fp16 (EngineWeights.raw16 is None)")
+        if on:
+            for r in raw:
+                for t, dt in ((r.w1, torch.float16), (r.w2, torch.float16), (r.g1, torch.float32),
+                              (r.g2, torch.float32)):
+                    if t.device != self.device or t.dtype != dt or not t.is_contiguous():
+                        raise ValueError("raw16 tensors must be contiguous fp16 (w1, w2) / fp32 (g1, g2) on the "
+                                         "model device")
+            arr = (_lib.CExact16Layer * self.cfg.n_layers)(
+                *[_lib.CExact16Layer(r.w1.data_ptr(), r.w2.data_ptr(), r.g1.data_ptr(), r.g2.data_ptr())
+                  for r in raw])
+            _lib.check(self._lib.tvr_model_set_exact16(self._h, arr), "tvr_model_set_exact16")
+            self._x16_c = arr
+        else:
+            _lib.check(self._lib.tvr_model_set_exact16(self._h, None), "tvr_model_set_exact16")
+            self._x16_c = None
+        self.exact16 = bool(on)
 
     def __del__(self):
         h = getattr(self, "_h", None)

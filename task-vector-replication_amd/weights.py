@@ -62,22 +62,27 @@ def hf_param_shapes(cfg: PythiaConfig) -> Dict[str, tuple]:
 
 
 def synth_param(cfg: PythiaConfig, name: str, shape: tuple, seed: int = 0,
-                device="cpu", std: float = 0.02, ln_std: float = 0.1) -> torch.Tensor:
+                device="cpu", std: float = 0.02, ln_std: float = 0.1, fp16: bool = False) -> torch.Tensor:
     """One seeded synthetic parameter (SURVEY.md §8d value distributions):
-    weights N(0, std), LayerNorm weights 1 + N(0, ln_std), biases N(0, std)."""
+    weights N(0, std), LayerNorm weights 1 + N(0, ln_std), biases N(0, std).
+    ``fp16``: rounded to fp16 values (held in fp32), as every tensor of the
+    released Pythia checkpoints is stored (their dtype is float16)."""
     g = torch.Generator(device=device)
     g.manual_seed(_seed_for(seed, name))
     x = torch.randn(shape, generator=g, device=device, dtype=torch.float32)
     if "layernorm" in name or "layer_norm" in name:
-        return (1.0 + ln_std * x) if name.endswith("weight") else x.mul_(std)
-    return x.mul_(std)
+        x = (1.0 + ln_std * x) if name.endswith("weight") else x.mul_(std)
+    else:
+        x = x.mul_(std)
+    return x.half().float() if fp16 else x
 
 
 def synth_hf_state_dict(cfg: PythiaConfig, seed: int = 0, device="cpu", std: float = 0.02,
-                        ln_std: float = 0.1) -> HFStateDict:
+                        ln_std: float = 0.1, fp16: bool = False) -> HFStateDict:
     """A full seeded synthetic HF-layout state dict (biases and LN params
-    non-trivial so fold_ln / fold_value_biases are exercised)."""
-    return {n: synth_param(cfg, n, s, seed, device, std, ln_std)
+    non-trivial so fold_ln / fold_value_biases are exercised); ``fp16`` as
+    :func:`synth_param`."""
+    return {n: synth_param(cfg, n, s, seed, device, std, ln_std, fp16)
             for n, s in hf_param_shapes(cfg).items()}
 
 
@@ -162,12 +167,25 @@ class EngineLayer:
 
 
 @dataclass
+class RawLayer16:
+    """One layer's checkpoint tensors for the exact-fp16 GEMMs (include/tvr.h
+    ``tvr_model_set_exact16``): W1 rows (Q | K | V in the engine order, then
+    MLP-in) and W2 = W_O | W_out BEFORE fold_ln / centring, as fp16 (exact:
+    built only from fp16-valued tensors), and LN1 / LN2 gamma (fp32)."""
+    w1: torch.Tensor   # fp16 [3d + d_mlp, d]
+    w2: torch.Tensor   # fp16 [d, d + d_mlp]
+    g1: torch.Tensor   # fp32 [d]
+    g2: torch.Tensor   # fp32 [d]
+
+
+@dataclass
 class EngineWeights:
     """Processed weights in the engine layout (all fp32, contiguous)."""
     w_embed: torch.Tensor          # [V, d]
     layers: List[EngineLayer]
     w_unembed_t: torch.Tensor      # [V, d]  (TL W_U transposed)
     b_unembed: torch.Tensor        # [V]
+    raw16: Optional[List[RawLayer16]] = None  # the exact-fp16 GEMM operands, when the checkpoint is fp16
 
     def tensors(self) -> List[torch.Tensor]:
         out = [self.w_embed, self.w_unembed_t, self.b_unembed]
@@ -176,7 +194,18 @@ class EngineWeights:
         return out
 
 
-def _process_layer(cfg: PythiaConfig, get) -> EngineLayer:
+def _exact16(*ts: torch.Tensor) -> bool:
+    """Every value of every tensor is an fp16 value (finite)."""
+    for t in ts:
+        h = t.half()
+        if not bool(torch.isfinite(h).all()) or not bool((h.float() == t).all()):
+            return False
+    return True
+
+
+def _process_layer(cfg: PythiaConfig, get, raw: Optional[list] = None) -> EngineLayer:
+    """One layer's TL processing.  ``raw`` (a list): the layer's RawLayer16 is
+    appended when its GEMM weights are exact in fp16, else None."""
     d, H, dh = cfg.d_model, cfg.n_heads, cfg.d_head
     ln1_w, ln1_b = get("input_layernorm.weight"), get("input_layernorm.bias")
     ln2_w, ln2_b = get("post_attention_layernorm.weight"), get("post_attention_layernorm.bias")
@@ -185,6 +214,14 @@ def _process_layer(cfg: PythiaConfig, get) -> EngineLayer:
     wqkv = get("attention.query_key_value.weight").view(H, 3, dh, d).transpose(0, 1).reshape(3 * d, d)
     bqkv = get("attention.query_key_value.bias").view(H, 3, dh).transpose(0, 1).reshape(3 * d)
     w_in, b_in = get("mlp.dense_h_to_4h.weight"), get("mlp.dense_h_to_4h.bias")
+    if raw is not None:
+        w_o_raw, w_out_raw = get("attention.dense.weight"), get("mlp.dense_4h_to_h.weight")
+        if _exact16(wqkv, w_in, w_o_raw, w_out_raw):
+            raw.append(RawLayer16(w1=torch.cat([wqkv, w_in], 0).half().contiguous(),
+                                  w2=torch.cat([w_o_raw, w_out_raw], 1).half().contiguous(),
+                                  g1=ln1_w.float().contiguous().clone(), g2=ln2_w.float().contiguous().clone()))
+        else:
+            raw.append(None)
     # fold_ln: biases first (they read the unscaled weights), then scale, then centre
     # the read-in weights over d_model.
     bqkv = bqkv + wqkv @ ln1_b
@@ -223,12 +260,31 @@ def _process_unembed(w_u: torch.Tensor, lnf_w: torch.Tensor, lnf_b: torch.Tensor
     return w_u.contiguous(), b_u.contiguous()
 
 
+# tensors _process_layer reads twice when raw16 is on (the raw copy and the processing)
+_RAW_NAMES = ("attention.query_key_value.weight", "mlp.dense_h_to_4h.weight", "attention.dense.weight",
+              "mlp.dense_4h_to_h.weight", "input_layernorm.weight", "post_attention_layernorm.weight")
+
+
+def _take_keep(sd, name, dev, dtype):
+    return sd[name].to(dev, dtype)
+
+
+def _raw_or_none(raw: Optional[list]) -> Optional[List[RawLayer16]]:
+    """The raw16 list when EVERY layer is exact in fp16, else None."""
+    if not raw or any(r is None for r in raw):
+        return None
+    return raw
+
+
 @torch.no_grad()
 def process_to_engine(cfg: PythiaConfig, sd: HFStateDict, device=None,
-                      free_source: bool = False, dtype=torch.float32) -> EngineWeights:
+                      free_source: bool = False, dtype=torch.float32, raw16: bool = True) -> EngineWeights:
     """TransformerLens ``process_weights_`` (fold_ln → center_writing_weights →
     center_unembed → fold_value_biases) straight into the engine layout.
-    ``free_source`` pops tensors from ``sd`` as it goes (bounds peak memory)."""
+    ``free_source`` pops tensors from ``sd`` as it goes (bounds peak memory).
+    ``raw16``: also keep the checkpoint's own GEMM weights as fp16 when every
+    one of them is exact in fp16 (released Pythia checkpoints are float16):
+    ``EngineWeights.raw16``, the operands of the exact-fp16 GEMMs."""
     dev = device if device is not None else sd["gpt_neox.embed_in.weight"].device
 
     def take(name):
@@ -237,31 +293,38 @@ def process_to_engine(cfg: PythiaConfig, sd: HFStateDict, device=None,
 
     w_e = take("gpt_neox.embed_in.weight")
     w_e = (w_e - w_e.mean(dim=1, keepdim=True)).contiguous()
-    layers = []
+    layers, raw = [], ([] if raw16 else None)
     for l in range(cfg.n_layers):
         p = f"gpt_neox.layers.{l}."
-        layers.append(_process_layer(cfg, lambda n, p=p: take(p + n)))
+        # the raw tensors are read before _process_layer pops them (free_source)
+        layers.append(_process_layer(cfg, lambda n, p=p: take(p + n) if not free_source or n not in _RAW_NAMES
+                                     else _take_keep(sd, p + n, dev, dtype), raw))
+        if free_source and raw is not None:
+            for n in _RAW_NAMES:
+                sd.pop(p + n, None)
     w_u, b_u = _process_unembed(take("embed_out.weight"), take("gpt_neox.final_layer_norm.weight"),
                                 take("gpt_neox.final_layer_norm.bias"))
-    return EngineWeights(w_e, layers, w_u, b_u)
+    return EngineWeights(w_e, layers, w_u, b_u, _raw_or_none(raw))
 
 
 @torch.no_grad()
 def synth_engine_weights(cfg: PythiaConfig, seed: int = 0, device="cpu", std: float = 0.02,
-                         ln_std: float = 0.1) -> EngineWeights:
+                         ln_std: float = 0.1, fp16: bool = False) -> EngineWeights:
     """Generate + process layer by layer (peak memory ~1 layer of raw weights),
-    the path used for the multi-GB configs on the GPU."""
+    the path used for the multi-GB configs on the GPU.  ``fp16``: every
+    parameter fp16-valued, as in the released checkpoints; the raw GEMM
+    weights are then kept too (``EngineWeights.raw16``)."""
     shapes = hf_param_shapes(cfg)
 
     def gen(name):
-        return synth_param(cfg, name, shapes[name], seed, device, std, ln_std)
+        return synth_param(cfg, name, shapes[name], seed, device, std, ln_std, fp16)
 
     w_e = gen("gpt_neox.embed_in.weight")
     w_e = (w_e - w_e.mean(dim=1, keepdim=True)).contiguous()
-    layers = []
+    layers, raw = [], ([] if fp16 else None)
     for l in range(cfg.n_layers):
         p = f"gpt_neox.layers.{l}."
-        layers.append(_process_layer(cfg, lambda n, p=p: gen(p + n)))
+        layers.append(_process_layer(cfg, lambda n, p=p: gen(p + n), raw))
     w_u, b_u = _process_unembed(gen("embed_out.weight"), gen("gpt_neox.final_layer_norm.weight"),
                                 gen("gpt_neox.final_layer_norm.bias"))
-    return EngineWeights(w_e, layers, w_u, b_u)
+    return EngineWeights(w_e, layers, w_u, b_u, _raw_or_none(raw))

@@ -34,13 +34,42 @@ def test_binding_covers_header():
 
 def test_version_and_errors_without_gpu():
     lib = tvr_amd._lib.load()
-    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 10
+    assert lib.tvr_abi_version() == tvr_amd._lib.ABI_VERSION == 11
     assert b"gfx950" in lib.tvr_version()
     # argument validation runs before any device call
     out = ctypes.c_void_p()
     rc = lib.tvr_model_create(None, None, None, None, None, ctypes.byref(out))
     assert rc == tvr_amd._lib.TVR_ERR_INVALID
     assert b"null" in lib.tvr_last_error()
+    assert lib.tvr_model_set_exact16(None, None) == tvr_amd._lib.TVR_ERR_INVALID
+
+
+def test_exact16_layer_record_matches_header():
+    text = (ROOT / "include" / "tvr.h").read_text()
+    body = re.search(r"typedef struct \{(.*?)\} tvr_exact16_layer;", text, re.S).group(1)
+    assert re.findall(r"\*\s*(\w+);", body) == [f for f, _ in tvr_amd._lib.CExact16Layer._fields_]
+
+
+def test_raw16_weights_only_for_fp16_values(tiny_cfg):
+    """weights.py keeps the checkpoint's own GEMM weights (fp16) only when every one is fp16-valued."""
+    import torch
+    w16 = tvr_amd.weights.synth_engine_weights(tiny_cfg, seed=0, fp16=True)
+    assert w16.raw16 is not None and len(w16.raw16) == tiny_cfg.n_layers
+    r = w16.raw16[0]
+    d, D1, K2 = tiny_cfg.d_model, 3 * tiny_cfg.d_model + tiny_cfg.d_mlp, tiny_cfg.d_model + tiny_cfg.d_mlp
+    assert r.w1.dtype == torch.float16 and tuple(r.w1.shape) == (D1, d)
+    assert r.w2.dtype == torch.float16 and tuple(r.w2.shape) == (d, K2)
+    assert r.g1.dtype == torch.float32 and tuple(r.g1.shape) == (d,)
+    # the processed W1 is fold_ln of the raw rows: W1' = W1 * gamma - row mean (TL fold_ln + centring)
+    w1p = r.w1.float().clone()
+    w1p[: 3 * d] = r.w1[: 3 * d].float() * r.g1
+    w1p[3 * d:] = r.w1[3 * d:].float() * r.g2
+    w1p = w1p - w1p.mean(dim=1, keepdim=True)
+    assert torch.allclose(w1p, w16.layers[0].w1, atol=1e-6, rtol=0)
+    # the processed W2 is the raw one centred over d_model
+    w2 = r.w2.float()
+    assert torch.allclose(w2 - w2.mean(dim=0, keepdim=True), w16.layers[0].w2, atol=1e-6, rtol=0)
+    assert tvr_amd.weights.synth_engine_weights(tiny_cfg, seed=0).raw16 is None
 
 
 def test_site_record_layout_matches_header():

@@ -52,12 +52,16 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 STD = 0.05
 TOL = 1e-4
 ARROW = tvr_amd.tasks.ARROW
-# model, asserted GEMM paths, reported-only paths, CIE layers, k-shot of the CIE prompt (T = 1 + 3k + 2)
+# model, asserted GEMM paths, reported-only paths, CIE layers, k-shot of the CIE prompt (T = 1 + 3k + 2),
+# fp16-valued weights (the released checkpoints' dtype: the x2f16 GEMMs then run on the exact fp16 weights,
+# 2 products, tests/test_gpu_exact16.py)
 FP32_MODELS = {
-    "2.8b": ("pythia-2.8b", ("x2f16", "f32"), (), (0, 16, 31), 4),
+    "2.8b": ("pythia-2.8b", ("x2f16", "f32"), (), (0, 16, 31), 4, False),
     # 12B f32: the exact-product fp32 MFMA path with the sliced accumulation (gemm_f32.hpp SLICE_KT; VERDICT r4:
     # unsliced it measured 2.7e-4 of max |CIE|, over the bar)
-    "12b": ("pythia-12b", ("x2f16", "f32"), (), (0, 18, 35), 10),
+    "12b": ("pythia-12b", ("x2f16", "f32"), (), (0, 18, 35), 10, False),
+    "2.8b-fp16w": ("pythia-2.8b", ("x2f16",), (), (0, 16, 31), 4, True),
+    "12b-fp16w": ("pythia-12b", ("x2f16",), (), (0, 18, 35), 10, True),
 }
 
 
@@ -66,12 +70,12 @@ def rel_err(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
-def streamed_oracle(cfg, std=STD):
+def streamed_oracle(cfg, std=STD, fp16=False):
     """fp64 oracle on cuda:0 over the SAME seeded weights the engine got
     (synth_param on the same device: identical fp32 values, then fp64)."""
     shapes = tvr_amd.weights.hf_param_shapes(cfg)
     return StreamedPythiaOracle(oracle_config(cfg),
-                                lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", std))
+                                lambda n: tvr_amd.weights.synth_param(cfg, n, shapes[n], 0, "cuda", std, fp16=fp16))
 
 
 class _Builder:  # the prompt builders need cfg, to_single_token and the tokenizer only
@@ -84,11 +88,12 @@ class _Builder:  # the prompt builders need cfg, to_single_token and the tokeniz
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("which", list(FP32_MODELS))
 def test_full_depth_fp32_paths(which):
-    name, gemms, reported, layers, kshot = FP32_MODELS[which]
+    name, gemms, reported, layers, kshot, fp16 = FP32_MODELS[which]
     cfg = tvr_amd.get_config(name)
     b = _Builder(cfg)
-    model = tvr_amd.Model.from_pretrained(name, device="cuda", seed=0, std=STD, gemm=gemms[0])
-    oracle = streamed_oracle(cfg)
+    model = tvr_amd.Model.from_pretrained(name, device="cuda", seed=0, std=STD, gemm=gemms[0], fp16_weights=fp16)
+    assert model.exact16 == fp16
+    oracle = streamed_oracle(cfg, fp16=fp16)
     heads = list(range(cfg.n_heads))
     try:
         prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(b, 1, kshot, seed=1234)

@@ -73,15 +73,18 @@ def model_task(oracle, xs, f):
     return out
 
 
-def reference(width):
-    """Oracle + everything the reference loops compute at this width (once)."""
-    if width in _CACHE:
-        return _CACHE[width]
+def reference(width, fp16=False):
+    """Oracle + everything the reference loops compute at this width (once).
+    ``fp16``: fp16-valued weights, as the released checkpoints (the engine then
+    binds its exact-fp16 GEMMs: tests/test_gpu_exact16.py)."""
+    key = (width, fp16)
+    if key in _CACHE:
+        return _CACHE[key]
     _CACHE.clear()
     name, L, n_prompts, kshot, n_ctx = WIDTHS[width]
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     cfg = tvr_amd.get_config(name).with_(n_layers=L)
-    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=STD)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=STD, fp16=fp16)
     tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
     oracle = make_oracle(cfg, sd, tok)
     letters = [x for x, _ in tvr_amd.tasks.letter_to_caps][:n_ctx]
@@ -105,7 +108,7 @@ def reference(width):
                                                          oracle)
     r["fv"] = R.assemble_task_vector(r["mean"], r["cie"], L - 1, 5) * 4  # x 4: it moves the top-5 at 2.8B width
     r["fv_acc"] = R.check_accuracy_of_task_vector(r["fv"], L - 1, r["colon"], 5, oracle)
-    _CACHE[width] = r
+    _CACHE[key] = r
     return r
 
 
@@ -113,8 +116,14 @@ def reference(width):
 @pytest.mark.parametrize("width,gemm", CASES, ids=[f"{w}-{g}" for w, g in CASES])
 def test_headline_width_parity(width, gemm):
     r = reference(width)
-    cfg, oracle = r["cfg"], r["oracle"]
-    model = tvr_amd.Model.from_hf_state_dict(cfg, r["sd"], device="cuda", tokenizer=r["tok"], gemm=gemm)
+    model = tvr_amd.Model.from_hf_state_dict(r["cfg"], r["sd"], device="cuda", tokenizer=r["tok"], gemm=gemm)
+    assert not model.exact16
+    check_width(r, model, gemm)
+
+
+def check_width(r, model, gemm):
+    """Every reference function at this width against the oracle's results in r."""
+    cfg = r["cfg"]
     bf16 = gemm == "bf16"
     tol = 2e-2 if bf16 else 1e-4
     try:

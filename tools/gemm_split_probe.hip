@@ -37,6 +37,11 @@ __global__ void fill_normal(float* p, size_t n, unsigned seed, float scale, int 
   }
 }
 
+__global__ void round_f16_kernel(float* p, size_t n) {  // weights exact in fp16 (a Pythia checkpoint's values)
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = (float)(_Float16)p[i];
+}
+
 __global__ void ref64(const float* A, const float* W, const int* rows, int nr, int N, int K, double* out, double* mag) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nr * N) return;
@@ -74,6 +79,9 @@ int main(int argc, char** argv) {
     hipMemset(wmax_bits, 0, 8);
     hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, A, (size_t)s.M * s.K, 11u, s.gelu ? 3.0f : 1.0f, s.gelu);
     hipLaunchKernelGGL(fill_normal, dim3(8192), dim3(256), 0, 0, W, (size_t)s.N * s.K, 29u, 0.02f, 0);
+    bool w16 = false;  // any one-plane-weight path: W exact in fp16 for every path of the run
+    for (const auto& p : paths) w16 = w16 || p.find("wx") != std::string::npos;
+    if (w16) hipLaunchKernelGGL(round_f16_kernel, dim3(8192), dim3(256), 0, 0, W, (size_t)s.N * s.K);
     hipLaunchKernelGGL(split_planes_kernel, dim3(8192), dim3(256), 0, 0, W, W3, (size_t)s.N * s.K);
     hipLaunchKernelGGL(absmax_kernel, dim3(2048), dim3(256), 0, 0, W, (size_t)s.N * s.K, wmax_bits);
     unsigned wb = 0;
@@ -141,15 +149,22 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12" || path == "x2pp13") {  // diagnostic variants
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12" || path == "x2pp13" || path == "x2pp15") {  // diagnostic variants
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
                     : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
                     : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
                     : path == "x2pp12" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 12>
                     : path == "x2pp13" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 13>
+                    : path == "x2pp15" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 15>
                                       : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 3>;
           hipLaunchKernelGGL(kp, dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2ppwx" || path == "x2ppslwx") {  // one-plane (exact fp16) weights, 2 products
+          grid = gemm_pingpong_grid(s.M, s.N);
+          auto kw = path == "x2ppwx" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, false, true>
+                                     : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true, true>;
+          hipLaunchKernelGGL(kw, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2ppsl" || path == "x2ppsl14" || path == "x2ppsl13") {  // sliced accumulation (6.9B / 12B)
           grid = gemm_pingpong_grid(s.M, s.N);
