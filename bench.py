@@ -771,6 +771,8 @@ def main():
     T = len(prompts[0])
     workload, scaling = describe_workload(args.model, cfg.n_layers, cfg.n_heads, args.prompts, args.kshot, T, world,
                                           shard, emulate, len(sites))
+    if model.exact16:  # another kernel instruction mix: counters of the 3-product runs do not apply
+        workload += ", fp16-valued weights (exact-fp16 GEMMs, 2 products)"
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     products = 2 if (args.gemm == "x2f16" and model.exact16) else PRODUCTS.get(args.gemm)
