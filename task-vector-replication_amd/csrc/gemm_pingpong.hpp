@@ -105,6 +105,11 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_SLICE_FORM
 #define TVR_PP_SLICE_FORM 2
 #endif
+// The sliced form with one-plane weights (WX): 1 the scheduled pairs below (tile 0's two products, then
+// tile 1's, the previous pair's adds two per MFMA gap), 0 the compiler-placed generic loop.
+#ifndef TVR_PP_SLICE_FORM_WX
+#define TVR_PP_SLICE_FORM_WX 1
+#endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
 // x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
@@ -416,6 +421,33 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   // phase's cluster (tc, for acc[ci][cj + 0..1]) and added there, while its first MFMAs run
   [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part, int ci, int cj) {
+#if TVR_PP_SLICE_FORM_WX == 1
+    if constexpr (FMT == ACT_X2F16 && SL && WX && !decltype(part)::value) {
+      // sliced, one-plane weights: per tile pair (i, 0..1) the tile-0 slice (a1 w0, then a0 w0 on it), then
+      // tile 1's, two of the previous pair's 8 slice-sum adds after each MFMA: the tile-0 sums a pair reads
+      // were finished 3 MFMAs before its first add, the tile-1 sums 3 before theirs (>= 9 issue slots: no
+      // s_nop before a read of an MFMA result); the last pair carried into the next phase (tc), as form 2
+      f32x4 t[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int di = i == 0 ? ci : i0 + i - 1, dj = i == 0 ? cj : j0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = q >> 1, pz = q & 1;  // MFMA q: product pz of tile j (0: a1 w0, 1: a0 w0)
+          t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][pz == 0 ? 1 : 0],
+                                                             pz == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : t[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+          for (int e = 2 * q; e < 2 * q + 2; ++e)
+            acc[di][dj + (e >> 2)][e & 3] += i == 0 ? tc[e >> 2][e & 3] : t[i - 1][e >> 2][e & 3];
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+      }
+      tc[0] = t[3][0];
+      tc[1] = t[3][1];
+      return;
+    }
+#endif
     if constexpr (FMT == ACT_X2F16 && SL && !WX && !decltype(part)::value) {
 #if TVR_PP_SLICE_FORM >= 1
       // tile pairs (i, 0..1) in turn — the pair's first products, second, third (two independent chains back
@@ -585,7 +617,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   if (vi == 8) {
     kloop(std::integral_constant<bool, false>{});
 #if TVR_PP_SLICE_FORM >= 1
-    if constexpr (FMT == ACT_X2F16 && SL && !WX) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
+    if constexpr (FMT == ACT_X2F16 && SL && (!WX || TVR_PP_SLICE_FORM_WX == 1)) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
       acc[7][0] = slice_add(acc[7][0], tc[0]);
       acc[7][1] = slice_add(acc[7][1], tc[1]);
     }
