@@ -25,6 +25,7 @@ import contextlib
 import ctypes
 import functools
 import inspect
+import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -67,15 +68,23 @@ def make_sites(n: int) -> np.ndarray:
 
 
 class Trace:
-    """Engine-owned clean-run snapshots (resid_pre per layer, z, K/V)."""
+    """Engine-owned clean-run snapshots (resid_pre per layer, z, K/V).
 
-    def __init__(self, model: "Model", max_seqs: int, max_tokens: int):
+    A caller's trace keeps its model alive; the experiment functions' scratch
+    trace (``weak``) does not, so ``del model`` frees the model's device memory
+    at once (no model <-> trace reference cycle waiting for the collector).
+    The model closes every live trace before it destroys itself."""
+
+    def __init__(self, model: "Model", max_seqs: int, max_tokens: int, weak: bool = False):
         self._lib = model._lib
+        self._h = None
         h = ctypes.c_void_p()
         _lib.check(self._lib.tvr_trace_create(model._h, max_seqs, max_tokens, ctypes.byref(h)),
                    "tvr_trace_create")
         self._h = h
-        self.model = model
+        self._model_strong = None if weak else model
+        self._model_ref = weakref.ref(model)
+        model._traces.add(self)
         self.max_seqs = max_seqs
         self.max_tokens = max_tokens
         self.seq_lens: List[int] = []
@@ -83,6 +92,13 @@ class Trace:
         # output tensors of a deferred clean forward, kept alive until the
         # engine has written them (the next patch sweep or trace read)
         self._pending_out = None
+
+    @property
+    def model(self) -> "Model":
+        m = self._model_strong if self._model_strong is not None else self._model_ref()
+        if m is None:
+            raise _lib.EngineError("the trace's model has been destroyed")
+        return m
 
     def resid_pre(self, layer: int) -> torch.Tensor:
         """``blocks.{layer}.hook_resid_pre`` of every traced token ([tokens, d]);
@@ -108,15 +124,21 @@ class Trace:
             _lib.check(self._lib.tvr_trace_flush(self._h, self.model._stream()), "tvr_trace_flush")
             self._pending_out = None
 
-    def __del__(self):
+    def close(self) -> None:
+        """Run a pending deferred forward (its outputs are owed to the caller)
+        and free the trace; idempotent.  Model.__del__ calls it on every live
+        trace of the model first, so no trace outlives its engine model."""
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             try:
                 if getattr(self, "_pending_out", None) is not None:
-                    self.flush()  # the deferred outputs are owed to the caller (tvr_trace_destroy would also run it)
+                    self.flush()  # (tvr_trace_destroy would also run it)
             finally:  # the device buffers are released even if the flush raised
-                self._lib.tvr_trace_destroy(h)
                 self._h = None
+                self._lib.tvr_trace_destroy(h)
+
+    def __del__(self):
+        self.close()
 
 
 # Matrix-core path of the GEMMs (Model.set_gemm): the fp32-accurate 2-plane
@@ -128,6 +150,7 @@ class Model(TokenizerMixin):
     def __init__(self, cfg: PythiaConfig, weights: EngineWeights, tokenizer=None,
                  device: Optional[torch.device] = None, gemm: str = DEFAULT_GEMM):
         self._h = None
+        self._traces = weakref.WeakSet()  # live traces of this model (closed before the model is destroyed)
         self._range_depth = 0
         self._lib = _lib.load()
         self._ops = _lib.load_ops()
@@ -251,9 +274,11 @@ class Model(TokenizerMixin):
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
+            for t in list(getattr(self, "_traces", ())):
+                t.close()  # before the engine model they point into is freed
             self._trace_cache = None
-            self._lib.tvr_model_destroy(h)
             self._h = None
+            self._lib.tvr_model_destroy(h)
 
     # ------------------------------------------------------------- internals
     def _stream(self) -> int:
@@ -302,7 +327,7 @@ class Model(TokenizerMixin):
             if t is not None:
                 t.flush()  # a deferral on the old trace still owes its outputs
             self._trace_cache = None
-            t = Trace(self, max(n_seqs, 1), max(n_tokens, 1))
+            t = Trace(self, max(n_seqs, 1), max(n_tokens, 1), weak=True)
             self._trace_cache = t
         return t
 

@@ -890,3 +890,27 @@ def test_deferred_clean_forward_runs_on_other_use(tiny_model):
     assert (clean2["prob"] - ref["prob"]).abs().max().item() <= 1e-6
     with pytest.raises(ValueError):
         tiny_model.forward_clean(prompts, trace=trace, defer=True, return_logits=True)
+
+
+def test_model_freed_on_del_and_traces_closed_first(tiny_cfg, tiny_sd, tokenizer):
+    """The experiment functions' scratch trace does not keep the model alive (no model <-> trace cycle: `del
+    model` frees it at once), and a caller's trace with a deferred forward pending is run and closed by the
+    model before the engine model is destroyed (never after, on a freed model)."""
+    import gc
+    import weakref
+    m = tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer)
+    mean = torch.randn(tiny_cfg.n_layers, tiny_cfg.n_heads, tiny_cfg.d_model, device="cuda") * 0.1
+    tvr_amd.experiments.causal_indirect_effect_sums(mean, [[0, 5, 9, 3]], [7], m)  # creates the scratch trace
+    assert m._trace_cache is not None
+    r = weakref.ref(m)
+    gc.disable()
+    try:
+        del m
+        assert r() is None  # freed by reference counting alone
+    finally:
+        gc.enable()
+    m = tvr_amd.Model.from_hf_state_dict(tiny_cfg, tiny_sd, device="cuda", tokenizer=tokenizer)
+    t = m.trace(1, 8)
+    out = m.forward_clean([[0, 5, 9, 3]], targets=[7], trace=t, defer=True)
+    m.__del__()  # as the collector would, with the trace still alive: the pending forward runs first
+    assert t._h is None and out["prob"].isfinite().all()
