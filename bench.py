@@ -130,6 +130,8 @@ def parse():
     ap.add_argument("--f32-leg", dest="f32_leg", action="store_true", default=True,
                     help="N=1: also time the sweep on the fp32 MFMA GEMM and compare CIE")
     ap.add_argument("--no-f32-leg", dest="f32_leg", action="store_false")
+    ap.add_argument("--no-processed-leg", dest="processed_leg", action="store_false", default=True,
+                    help="skip the 3-product re-timing on the processed weights (profiling runs)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI) for real runs; gloo to rehearse several ranks on one GPU")
     ap.add_argument("--configs", default="C2,C4,C5",
@@ -856,7 +858,7 @@ def main():
     out["config"]["gemm"] = args.gemm
     out["config"]["weights"] = args.weights
     out["config"]["exact16_gemms"] = bool(model.exact16)
-    if world == 1 and model.exact16 and not emulate:
+    if world == 1 and model.exact16 and not emulate and args.processed_leg:
         # the same sweep on the TL-processed weights (3 products: the path of fp32-valued checkpoints)
         model.set_exact16(False)
         npw = max(1, min(args.steps, 2))
