@@ -176,6 +176,14 @@ typedef struct {
   const float* g2;
 } tvr_exact16_layer;
 int tvr_model_set_exact16(tvr_model* model, const tvr_exact16_layer* layers /*[n_layers] host, or NULL*/);
+/* The unembed's part of the exact-fp16 binding (X2F16 mode, with the layers
+ * bound): wu fp16 [d_vocab][d_model] = the checkpoint's embed_out.weight
+ * BEFORE fold_ln / center_unembed, gf fp32 [d_model] = the final LN's gamma.
+ * The patch sweeps' fused-statistics unembed then reads LNPre(x) * gf against
+ * wu (2 products); the omitted centring over the vocabulary is one constant per
+ * row of logits, which softmax probabilities and top-k do not see.  Paths that
+ * return logits keep the processed W_U.  NULL, NULL detaches. */
+int tvr_model_set_exact16_unembed(tvr_model* model, const uint16_t* wu, const float* gf);
 
 /* Clean-run trace: every layer's hook_resid_pre, attn.hook_z and the K/V
  * inputs, the state run_with_cache keeps (scratch2.py:96, scratch.py:132,137). */

@@ -113,6 +113,7 @@ SIGNATURES = {
     "tvr_workspace_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
     "tvr_model_set_gemm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]),
     "tvr_model_set_exact16": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tvr_model_set_exact16_unembed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tvr_model_get_gemm": (ctypes.c_int32, [ctypes.c_void_p]),
     "tvr_split_planes": (ctypes.c_int, [c_f32p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "tvr_gemm_x3bf16": (ctypes.c_int, [c_f32p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,

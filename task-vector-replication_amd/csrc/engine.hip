@@ -161,6 +161,12 @@ struct tvr_model {
   bool x16 = false;
   std::vector<MatW> w1x, w2x;
   std::vector<const float*> g1, g2;
+  // the unembed's raw W_U [V][d] (one fp16 plane) and the final LN's gamma (tvr_model_set_exact16_unembed): the
+  // fused-statistics unembed reads LNPre(x) * gf against it (2 products).  fold_ln's centring is a no-op again,
+  // and center_unembed's mean over the vocabulary is one constant per row of logits, which the statistics
+  // (softmax probability, top-k) do not see; the logits paths keep the processed W_U.
+  MatW wux;
+  const float* gf = nullptr;
 };
 
 struct tvr_trace {
@@ -374,13 +380,13 @@ void launch_pp(int epi, const uint16_t* Ah, int lda, int a_fmt, const MatW& W, i
   switch (epi) {
     case EPI_BIAS: TVR_PP1F(EPI_BIAS); break;
     case EPI_SPLIT_GELU_ACT: TVR_PP1F(EPI_SPLIT_GELU_ACT); break;
-    case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked; never one-plane weights)
+    case EPI_STATS:  // LDS epilogue only (vec: N % 4 == 0, host-checked)
       if (a_fmt != ACT_X2F16) {
         TVR_PP1(EPI_STATS, ACT_BF16, true, false, false);
       } else if (sl) {
-        TVR_PP1(EPI_STATS, ACT_X2F16, true, true, false);
+        if (wx) { TVR_PP1(EPI_STATS, ACT_X2F16, true, true, true); } else { TVR_PP1(EPI_STATS, ACT_X2F16, true, true, false); }
       } else {
-        TVR_PP1(EPI_STATS, ACT_X2F16, true, false, false);
+        if (wx) { TVR_PP1(EPI_STATS, ACT_X2F16, true, false, true); } else { TVR_PP1(EPI_STATS, ACT_X2F16, true, false, false); }
       }
       break;
     default: TVR_PP1F(EPI_RESID); break;
@@ -675,8 +681,8 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
                                  "statistics buffer");
   if (a_fmt == ACT_F16 && epi != EPI_BIAS)
     return fail(TVR_ERR_INVALID, "gemm: the fp16 operand format has the plain (bias) epilogue only");
-  if (W.x16 && (a_fmt != ACT_X2F16 || epi == EPI_STATS))
-    return fail(TVR_ERR_INVALID, "gemm: one-plane exact fp16 weights take x2f16 activations and no statistics epilogue");
+  if (W.x16 && a_fmt != ACT_X2F16)
+    return fail(TVR_ERR_INVALID, "gemm: one-plane exact fp16 weights take x2f16 activations");
   if (ep.a2 && (a_fmt == ACT_F32 || ep.a2_col % 256 != 0))
     return fail(TVR_ERR_INVALID, "gemm: a second A operand needs a planar format and a 256-column boundary");
   if (K % GEMM_BK != 0 || lda % 4 != 0 || ldw % 4 != 0 || ((W.x || W.h) && ldw % 8 != 0) ||
@@ -928,8 +934,8 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   ProfSpan ps(m, st);
   if (d % 4 != 0 || ldx % 4 != 0 || ldy % 4 != 0)
     return fail(TVR_ERR_UNSUPPORTED, "lnpre: d and strides must be multiples of 4");
-  if (g1 && (fmt != ACT_X2F16 || !g2 || !y2 || !m))
-    return fail(TVR_ERR_INTERNAL, "lnpre: the gamma-scaled pair is an x2f16 model path");
+  if (g1 && (fmt != ACT_X2F16 || (y2 && !g2) || !m))
+    return fail(TVR_ERR_INTERNAL, "lnpre: the gamma-scaled rows are an x2f16 model path");
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
   if (fmt == ACT_X2F16)
@@ -944,7 +950,7 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
   TVR_HIP(hipGetLastError());
   // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element;
   // the gamma-scaled pair two x2f16 rows)
-  ps.done(TVR_HBM_LNPRE, (double)rows * d * (g1 ? 12.0 : 8.0) +
+  ps.done(TVR_HBM_LNPRE, (double)rows * d * (y2 ? 12.0 : 8.0) +
                              (copy ? (double)std::min(rows, copy_rows) * d * 4.0 : 0.0));
   return TVR_OK;
 }
@@ -1255,7 +1261,9 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
   const int tiles = (V + 255) / 256, chunk = final_chunk(m, fmt, out_logits);
   for (int s = 0; s < n; s += chunk) {
     const int cn = std::min(chunk, n - s);
-    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m));
+    const bool xu = fused && use_x16(m) && m->wux.h;  // the exact-fp16 unembed (statistics only)
+    TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m, nullptr, nullptr, 0,
+                         xu ? m->gf : nullptr));
     if (fused) {
       float* part = scratch;
       float* tlogit = scratch + (size_t)cn * tiles * (2 + 2 * topk);
@@ -1266,7 +1274,7 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
       e.stats_tiles = tiles;
       e.targets = d_targets ? d_targets + s : nullptr;
       e.tlogit = tlogit;
-      TVR_TRY(launch_gemm(EPI_STATS, xf, d, fmt, m->wu, d, cn, V, d, e, st, m));
+      TVR_TRY(launch_gemm(EPI_STATS, xf, d, fmt, xu ? m->wux : m->wu, d, cn, V, d, e, st, m));
       ProfSpan ps(m, st);
       hipLaunchKernelGGL(stats_merge_kernel, dim3((cn + MERGE_WAVES - 1) / MERGE_WAVES), dim3(64 * MERGE_WAVES), 0,
                          st, part, tiles, topk, tlogit, d_targets ? d_targets + s : nullptr, cn, V,
@@ -1409,6 +1417,14 @@ static int replan_x2f16(tvr_model* m) {
   if (m->gemm_mode != TVR_GEMM_X2F16) return TVR_OK;
   TVR_TRY(tvr_model_set_gemm(m, TVR_GEMM_F32, nullptr));
   return tvr_model_set_gemm(m, TVR_GEMM_X2F16, nullptr);
+}
+
+int tvr_model_set_exact16_unembed(tvr_model* m, const uint16_t* wu, const float* gf) {
+  if (!m) return fail(TVR_ERR_INVALID, "tvr_model_set_exact16_unembed: null model");
+  if (!wu != !gf) return fail(TVR_ERR_INVALID, "tvr_model_set_exact16_unembed: give both arrays or neither");
+  m->wux = wu ? MatW{nullptr, nullptr, wu, 0, 1.0f, true} : MatW{};
+  m->gf = gf;
+  return TVR_OK;
 }
 
 int tvr_model_set_exact16(tvr_model* m, const tvr_exact16_layer* layers) {

@@ -110,6 +110,12 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_SLICE_FORM_WX
 #define TVR_PP_SLICE_FORM_WX 1
 #endif
+// One-plane weights: 1 stage the 2-piece activation regions in the read-light phases (pp_tile), 0 (default)
+// the 3-product order.  Measured within noise (qkv / o probe shapes 654 / 672 vs 651 / 671 TF, sliced 578 /
+// 582 vs 578 / 580, identical results: profiles/r05/wx_stage_ab_r05ab.txt), so the proven order stays.
+#ifndef TVR_PP_WX_STAGE
+#define TVR_PP_WX_STAGE 0
+#endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
 // x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
@@ -556,13 +562,27 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   __builtin_amdgcn_sched_barrier(0)
 
   // ---- prologue: the stage history of tiles -2 and -1 in loop order (A_lo W_lo
-  // A_hi W_hi of tile 0, A_lo W_lo of tile 1), then retire A_lo(0) / W_lo(0)
-  stage(0, 0);
-  stage(2, 0);
-  stage(1, 0);
-  stage(3, 0);
-  stage(0, 1);
-  stage(2, 1);
+  // A_hi W_hi of tile 0, A_lo W_lo of tile 1), then retire A_lo(0) / W_lo(0).
+  // One-plane weights (WX, TVR_PP_WX_STAGE): a weight region is 1 piece per wave and an activation region 2,
+  // so the 2-piece regions are staged in the phases with few fragment reads (q2: 2 reads, q4: none) and the
+  // 1-piece ones in the read-heavy q1 / q3:  q1 W_hi(t+1), q2 A_hi(t+1), q3 W_lo(t+2), q4 A_lo(t+2) — each
+  // still >= 2 phases after its region's last read and retired one phase before its first
+  constexpr bool XS = WX && TVR_PP_WX_STAGE;
+  if constexpr (XS) {
+    stage(2, 0);
+    stage(0, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(2, 1);
+    stage(0, 1);
+  } else {
+    stage(0, 0);
+    stage(2, 0);
+    stage(1, 0);
+    stage(3, 0);
+    stage(0, 1);
+    stage(2, 1);
+  }
   // counted waits: the pieces issued after the awaited region (2 per wave per region; 1 for a WX weight region)
   if constexpr (WX)
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -584,33 +604,45 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       // q1: Q(A_lo, W_lo)
       read_a(cur, 0, part);
       read_w(cur, 0, fwl, part);
-      if constexpr (WX) {
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if constexpr (XS) {
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // W_hi(kt) (q1 of kt-1), read in q2
+        stage(3, kt + 1);
       } else {
-        if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
+        if constexpr (WX) {
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+          if (VAR != 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // W_hi(kt) (issued in q2 of kt-1), read in q2
+        }
+        stage(1, kt + 1);
       }
-      stage(1, kt + 1);
       TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part, 7, 0));  // (ci, cj): the carried pair of the previous phase
       // q2: Q(A_lo, W_hi)
       read_w(cur, 2, fwh, part);
-      if constexpr (WX) {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (XS) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A_hi(kt) (q2 of kt-1), read in q3
+        stage(1, kt + 1);
       } else {
-        if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+        if constexpr (WX) {
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          if (VAR != 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+        }
+        stage(3, kt + 1);
       }
-      stage(3, kt + 1);
       TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part, 3, 0));
       // q3: Q(A_hi, W_hi)
       read_a(cur, 4, part);
-      stage(0, kt + 2);
+      stage(XS ? 2 : 0, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part, 3, 2));
       // q4: Q(A_hi, W_lo)
-      if constexpr (WX) {
+      if constexpr (XS) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A_lo(kt+1) (q4 of kt-1), W_lo(kt+1) (q3 of kt-1), read in q1
+      } else if constexpr (WX) {
         asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       } else {
         if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
       }
-      stage(2, kt + 2);
+      stage(XS ? 0 : 2, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part, 7, 2));
     }
   };

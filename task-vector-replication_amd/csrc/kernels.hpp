@@ -88,8 +88,9 @@ __global__ void center_rows_kernel(const float* __restrict__ src, float* __restr
 // fp32 (ACT_F32) or a planar activation format (split.hpp; ldy counts logical
 // elements); the outputs are bounded by sqrt(d), so no range check.
 constexpr int LN_REG_F4 = 20;  // float4 per lane held in registers: d <= 5120 (Pythia-12B), d % 256 == 0
-// g1 (x2f16, engine.hip's exact-fp16 weights): y = LNPre(x) * g1 and y2 = LNPre(x) * g2 instead (LN1's
-// and LN2's gamma, the read-in weights' fold_ln scale moved onto the rows), range-checked into flag.
+// g1 (x2f16, engine.hip's exact-fp16 weights): y = LNPre(x) * g1 and, with y2, y2 = LNPre(x) * g2 instead
+// (LN1's and LN2's gamma, or the final LN's alone: the read-in weights' fold_ln scale moved onto the rows),
+// range-checked into flag.
 template <int FMT>
 __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
@@ -132,20 +133,23 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     const float scale = sqrtf(wave_sum(ss) / (float)d + eps);
     if (stats && lane == 0) stats[r] = make_float2(mean, scale);
     if constexpr (FMT == ACT_X2F16) {
-      if (g1) {  // the two gamma-scaled rows
+      if (g1) {  // the gamma-scaled row(s): y = x g1 (and y2 = x g2 when y2 is given)
         float mx = 0.f;
 #pragma unroll
         for (int u = 0; u < LN_REG_F4; ++u) {
           if (u < nv) {
             const int c = lane + 64 * u;
             const float4 o = make_float4(v[u].x / scale, v[u].y / scale, v[u].z / scale, v[u].w / scale);
-            const float4 a = ((const float4*)g1)[c], b = ((const float4*)g2)[c];
+            const float4 a = ((const float4*)g1)[c];
             const float4 p = make_float4(o.x * a.x, o.y * a.y, o.z * a.z, o.w * a.w);
-            const float4 q = make_float4(o.x * b.x, o.y * b.y, o.z * b.z, o.w * b.w);
             store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
-            store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
-            mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
-                                 fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w)))));
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
+            if (y2) {
+              const float4 b = ((const float4*)g2)[c];
+              const float4 q = make_float4(o.x * b.x, o.y * b.y, o.z * b.z, o.w * b.w);
+              store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
+              mx = fmaxf(mx, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+            }
           }
         }
         if (mx * X2_ASCALE >= X2_FP16_OVERFLOW && flag) atomicOr(flag, 1u);
@@ -188,13 +192,16 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
     v.z = (v.z - mean) / scale; v.w = (v.w - mean) / scale;
     if constexpr (FMT == ACT_X2F16) {
       if (g1) {
-        const float4 a = ((const float4*)g1)[c], b = ((const float4*)g2)[c];
+        const float4 a = ((const float4*)g1)[c];
         const float4 p = make_float4(v.x * a.x, v.y * a.y, v.z * a.z, v.w * a.w);
-        const float4 q = make_float4(v.x * b.x, v.y * b.y, v.z * b.z, v.w * b.w);
         store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
-        store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
-        mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))),
-                             fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w)))));
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
+        if (y2) {
+          const float4 b = ((const float4*)g2)[c];
+          const float4 q = make_float4(v.x * b.x, v.y * b.y, v.z * b.z, v.w * b.w);
+          store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
+          mx = fmaxf(mx, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+        }
         continue;
       }
     }

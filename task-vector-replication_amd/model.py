@@ -266,7 +266,16 @@ class Model(TokenizerMixin):
                   for r in raw])
             _lib.check(self._lib.tvr_model_set_exact16(self._h, arr), "tvr_model_set_exact16")
             self._x16_c = arr
+            ru = self.weights.raw16_unembed
+            if ru is not None:
+                wu, gf = ru
+                if wu.device != self.device or wu.dtype != torch.float16 or not wu.is_contiguous() or \
+                        gf.device != self.device or gf.dtype != torch.float32:
+                    raise ValueError("raw16_unembed must be (fp16 [V, d], fp32 [d]) contiguous on the model device")
+                _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, wu.data_ptr(), gf.data_ptr()),
+                           "tvr_model_set_exact16_unembed")
         else:
+            _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, None, None), "tvr_model_set_exact16_unembed")
             _lib.check(self._lib.tvr_model_set_exact16(self._h, None), "tvr_model_set_exact16")
             self._x16_c = None
         self.exact16 = bool(on)

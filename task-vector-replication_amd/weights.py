@@ -186,6 +186,8 @@ class EngineWeights:
     w_unembed_t: torch.Tensor      # [V, d]  (TL W_U transposed)
     b_unembed: torch.Tensor        # [V]
     raw16: Optional[List[RawLayer16]] = None  # the exact-fp16 GEMM operands, when the checkpoint is fp16
+    # the unembed's: the checkpoint's embed_out.weight (fp16 [V, d]) and the final LN gamma (fp32 [d])
+    raw16_unembed: Optional[tuple] = None
 
     def tensors(self) -> List[torch.Tensor]:
         out = [self.w_embed, self.w_unembed_t, self.b_unembed]
@@ -269,6 +271,11 @@ def _take_keep(sd, name, dev, dtype):
     return sd[name].to(dev, dtype)
 
 
+def _raw_unembed(wu: torch.Tensor, gf: torch.Tensor) -> Optional[tuple]:
+    """(embed_out.weight as fp16, final LN gamma) when the unembed is exact in fp16, else None."""
+    return (wu.half().contiguous(), gf.float().contiguous().clone()) if _exact16(wu) else None
+
+
 def _raw_or_none(raw: Optional[list]) -> Optional[List[RawLayer16]]:
     """The raw16 list when EVERY layer is exact in fp16, else None."""
     if not raw or any(r is None for r in raw):
@@ -302,9 +309,11 @@ def process_to_engine(cfg: PythiaConfig, sd: HFStateDict, device=None,
         if free_source and raw is not None:
             for n in _RAW_NAMES:
                 sd.pop(p + n, None)
-    w_u, b_u = _process_unembed(take("embed_out.weight"), take("gpt_neox.final_layer_norm.weight"),
-                                take("gpt_neox.final_layer_norm.bias"))
-    return EngineWeights(w_e, layers, w_u, b_u, _raw_or_none(raw))
+    wu_raw, gf = take("embed_out.weight"), take("gpt_neox.final_layer_norm.weight")
+    raw_u = _raw_unembed(wu_raw, gf) if raw16 else None
+    w_u, b_u = _process_unembed(wu_raw, gf, take("gpt_neox.final_layer_norm.bias"))
+    raw = _raw_or_none(raw)
+    return EngineWeights(w_e, layers, w_u, b_u, raw, raw_u if raw is not None else None)
 
 
 @torch.no_grad()
@@ -325,6 +334,8 @@ def synth_engine_weights(cfg: PythiaConfig, seed: int = 0, device="cpu", std: fl
     for l in range(cfg.n_layers):
         p = f"gpt_neox.layers.{l}."
         layers.append(_process_layer(cfg, lambda n, p=p: gen(p + n), raw))
-    w_u, b_u = _process_unembed(gen("embed_out.weight"), gen("gpt_neox.final_layer_norm.weight"),
-                                gen("gpt_neox.final_layer_norm.bias"))
-    return EngineWeights(w_e, layers, w_u, b_u, _raw_or_none(raw))
+    wu_raw, gf = gen("embed_out.weight"), gen("gpt_neox.final_layer_norm.weight")
+    raw_u = _raw_unembed(wu_raw, gf) if fp16 else None
+    w_u, b_u = _process_unembed(wu_raw, gf, gen("gpt_neox.final_layer_norm.bias"))
+    raw = _raw_or_none(raw)
+    return EngineWeights(w_e, layers, w_u, b_u, raw, raw_u if raw is not None else None)

@@ -42,6 +42,7 @@ def test_version_and_errors_without_gpu():
     assert rc == tvr_amd._lib.TVR_ERR_INVALID
     assert b"null" in lib.tvr_last_error()
     assert lib.tvr_model_set_exact16(None, None) == tvr_amd._lib.TVR_ERR_INVALID
+    assert lib.tvr_model_set_exact16_unembed(None, None, None) == tvr_amd._lib.TVR_ERR_INVALID
 
 
 def test_exact16_layer_record_matches_header():
@@ -69,6 +70,8 @@ def test_raw16_weights_only_for_fp16_values(tiny_cfg):
     # the processed W2 is the raw one centred over d_model
     w2 = r.w2.float()
     assert torch.allclose(w2 - w2.mean(dim=0, keepdim=True), w16.layers[0].w2, atol=1e-6, rtol=0)
+    wu, gf = w16.raw16_unembed
+    assert wu.dtype == torch.float16 and tuple(wu.shape) == (tiny_cfg.d_vocab, d) and gf.dtype == torch.float32
     assert tvr_amd.weights.synth_engine_weights(tiny_cfg, seed=0).raw16 is None
 
 
