@@ -116,6 +116,10 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_WX_STAGE
 #define TVR_PP_WX_STAGE 0
 #endif
+// One-plane weights, unsliced: 1 the two-phase, three-buffer K loop (pp_tile P2), 0 the four-phase one
+#ifndef TVR_PP_WX_2PHASE
+#define TVR_PP_WX_2PHASE 0
+#endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
 // x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
@@ -327,13 +331,20 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   static_assert(!WX || FMT == ACT_X2F16, "one-plane weights: x2f16 activations only");
   constexpr int WNPL = WX ? 1 : NPL;   // weight planes staged
   constexpr int BUF = (NPL + WNPL) * PL; // halves per buffer: A planes, then W planes
-  constexpr int DUMMY = 2 * BUF;       // 1 KB staging sink past the last k-tile
+  // P2 (one-plane weights, unsliced, TVR_PP_WX_2PHASE): 2 phases per k-tile of 32 MFMAs each and 3 LDS
+  // buffers (3 x 48 KB: the one-plane buffer is 3/4 of the two-plane one), kloop below
+  constexpr bool P2 = WX && !SL && TVR_PP_WX_2PHASE;
+  constexpr int NBUF = P2 ? 3 : 2;
+  constexpr int DUMMY = NBUF * BUF;    // 1 KB staging sink past the last k-tile
+  constexpr int LDS_HALVES = P2 ? (NBUF * BUF + 512 > PP_EPI_LDS ? NBUF * BUF + 512 : PP_EPI_LDS)
+                                : PpLds<FMT>::HALVES;
+  static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget (P2)");
   static_assert(NPL * KG == 2, "two fragments per 16-row slice per k-tile");
   static_assert(PpLds<FMT>::HALVES * 2 <= 160 * 1024, "LDS budget");
   // ONE __shared__ object (a second one can make hipcc drain vmcnt before
   // ds_reads), declared here so every access is a known LDS address (a
   // generic pointer parameter costs VGPRs: 64-bit flat addresses)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[PpLds<FMT>::HALVES];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_HALVES];
 
   // the thread index through an empty asm: a stream-K block's two inlined
   // tiles then recompute their lane addresses instead of one copy holding the
@@ -379,7 +390,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     if (VAR == 1 && kt >= 2) return;
     const bool live = kt < nk;
     const int koff = live && VAR != 12 ? (kbeg + kt) * BK : 0;  // VAR 12: every k-tile re-reads k-tile 0 (L2-hot)
-    const int boff = (kt & 1) * BUF;
+    const int boff = (P2 ? kt % 3 : kt & 1) * BUF;
 #pragma unroll
     for (int s = 0; s < ((WX && R >= 2) ? 1 : 2); ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
   };
@@ -567,8 +578,19 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   // so the 2-piece regions are staged in the phases with few fragment reads (q2: 2 reads, q4: none) and the
   // 1-piece ones in the read-heavy q1 / q3:  q1 W_hi(t+1), q2 A_hi(t+1), q3 W_lo(t+2), q4 A_lo(t+2) — each
   // still >= 2 phases after its region's last read and retired one phase before its first
-  constexpr bool XS = WX && TVR_PP_WX_STAGE;
-  if constexpr (XS) {
+  constexpr bool XS = WX && TVR_PP_WX_STAGE && !P2;
+  if constexpr (P2) {
+    // tiles 0 and 1 in loop order (R1: A_lo, W_lo, W_hi; R2: A_hi), then retire tile 0's R1 regions:
+    // 2 + 4 + 2 pieces issued after them
+    stage(0, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(0, 1);
+    stage(2, 1);
+    stage(3, 1);
+    stage(1, 1);
+  } else if constexpr (XS) {
     stage(2, 0);
     stage(0, 0);
     stage(3, 0);
@@ -584,7 +606,9 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     stage(2, 1);
   }
   // counted waits: the pieces issued after the awaited region (2 per wave per region; 1 for a WX weight region)
-  if constexpr (WX)
+  if constexpr (P2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (WX)
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -599,6 +623,30 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   unsigned long long d_loop0 = 0, d_loop1 = 0;
   if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
   auto kloop = [&](auto part) {
+    if constexpr (P2) {
+      // k-tile kt in 3-buffer rotation; per wave group: R1 [read A_lo, W_lo, W_hi; retire A_hi(kt); stage
+      // A_lo / W_lo / W_hi of kt + 2] barrier [32 MFMAs: rows 0-63] barrier, R2 [read A_hi; retire the R1
+      // regions of kt + 1; stage A_hi(kt + 2)] barrier [32 MFMAs: rows 64-127] barrier.  Buffer (kt + 2) % 3
+      // held k-tile kt - 1, whose last reads (the lagging group's, one segment late) are >= 3 segments
+      // before these stages; every region is retired one phase before its first read and >= 3 segments
+      // after it was issued (counted waits: 4 + 2 pieces issued since)
+      for (int kt = 0; kt < nk; ++kt) {
+        const uint16_t* cur = lds + (kt % 3) * BUF;
+        read_a(cur, 0, part);
+        read_w(cur, 0, fwl, part);
+        read_w(cur, 2, fwh, part);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_hi(kt) (R2 of kt - 2), read in R2
+        stage(0, kt + 2);
+        stage(2, kt + 2);
+        stage(3, kt + 2);
+        TVR_PP_CLUSTER(mfma_quadrant(0, 0, fwl, part, 7, 0); mfma_quadrant(0, 2, fwh, part, 3, 0));
+        read_a(cur, 4, part);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo, W_lo, W_hi of kt + 1 (R1 of kt - 1)
+        stage(1, kt + 2);
+        TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part, 7, 2); mfma_quadrant(4, 2, fwh, part, 3, 2));
+      }
+      return;
+    }
     for (int kt = 0; kt < nk; ++kt) {
       const uint16_t* cur = lds + (kt & 1) * BUF;
       // q1: Q(A_lo, W_lo)
