@@ -352,9 +352,11 @@ int tvr_profile_read_hbm(tvr_model* model, tvr_hbm_stats* out);
  * the QKV + MLP-in launch (GELU epilogue); bit 1 (TVR_PLAN_MODEL_SLICED): the
  * launch belongs to a model whose O + MLP-out K reaches the sliced-accumulation
  * threshold (6.9B, 12B: every x2f16 GEMM of such a model runs sliced, as does
- * any launch with K >= that threshold).  Host-only, no device call
- * (diagnostics, CPU tests).  (ABI 10; flag bit 1 from round 5) */
-enum { TVR_PLAN_GELU = 1, TVR_PLAN_MODEL_SLICED = 2 };
+ * any launch with K >= that threshold); bit 2 (TVR_PLAN_EXACT16): one exact
+ * fp16 weight plane (tvr_model_set_exact16: 2 products, cheaper k-tiles).
+ * Host-only, no device call (diagnostics, CPU tests).  (ABI 10; flag bits 1
+ * and 2 from round 5) */
+enum { TVR_PLAN_GELU = 1, TVR_PLAN_MODEL_SLICED = 2, TVR_PLAN_EXACT16 = 4 };
 int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t flags, int32_t* out);
 
 /* Bytes of engine workspace currently held by the model (diagnostics);

@@ -578,11 +578,14 @@ double plan_reduce_us(int M, int N, int t0, int cnt, int S) {
   return 4.0 + rows * 4.0 * (2.0 * S + 1.0) / 5.0e6;  // partials written (by the GEMM) + read, output written
 }
 
-// sliced: the launch runs the x2f16 sliced accumulation (~13 % more per k-tile: gemm_pingpong.hpp)
-PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
+// sliced: the launch runs the x2f16 sliced accumulation (~13 % more per k-tile: gemm_pingpong.hpp); wx: one
+// exact weight plane, 2 products (0.72 of the 3-product k-tile, 0.85 sliced: profiles/r05/wx_probe_r05r.jsonl)
+PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false, bool wx = false) {
   PpPlan p;
   const int tiles = gemm_pingpong_grid(M, N), nkt = K / (a_fmt == ACT_X2F16 ? 32 : 64);
-  const double kt_us = (a_fmt == ACT_X2F16 ? 1.9 : 1.3) * (sliced ? 1.13 : 1.0), seg_us = 15.0, epi_us = 10.0;
+  const double kt_scale = wx ? (sliced ? 0.85 : 0.72) : 1.0;
+  const double kt_us = (a_fmt == ACT_X2F16 ? 1.9 : 1.3) * (sliced ? 1.13 : 1.0) * kt_scale, seg_us = 15.0,
+               epi_us = 10.0;
   // stream-K of `cnt` tiles over min(256, iterations) blocks vs one plain round
   auto sk_us = [&](int cnt) {
     const int G = (int)std::min<long long>(256, (long long)cnt * nkt);
@@ -637,7 +640,7 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
     }
   }
   if (best < 2) return p;
-  const double round_us = nkt * 2.5;  // ~2.3-2.7 us per k-tile per block (profiles/gemm_pingpong_anatomy_r01.jsonl)
+  const double round_us = nkt * 2.5 * kt_scale;  // ~2.3-2.7 us per k-tile per block (profiles/gemm_pingpong_anatomy_r01.jsonl)
   const double saved_us = (1.0 - br) * round_us;
   const double cost_us = (best + 1.0) * tb * (double)PP_TILE_ELEMS * 8.0 / 5.0e6;  // partials written + read, ~5 TB/s
   if (saved_us > 1.5 * cost_us + 10.0) {
@@ -649,11 +652,12 @@ PpPlan plan_pp(int M, int N, int K, int a_fmt, int epi, bool sliced = false) {
 
 // plan_pp, cached per launch shape on the model (the sweeps repeat their
 // per-layer shapes: the simulation runs once per shape)
-PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi) {
-  const PlanKey key{M, N, K, a_fmt, epi == EPI_SPLIT_GELU_ACT ? 1 : epi == EPI_RESID ? 2 : 0, sk_mode()};
+PpPlan plan_pp_cached(tvr_model* m, int M, int N, int K, int a_fmt, int epi, bool wx = false) {
+  const PlanKey key{M, N, K, a_fmt + (wx ? 16 : 0), epi == EPI_SPLIT_GELU_ACT ? 1 : epi == EPI_RESID ? 2 : 0, sk_mode()};
   auto it = m->plans.find(key);
   if (it != m->plans.end()) return it->second;
-  const PpPlan p = plan_pp(M, N, K, a_fmt, epi, a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || m->K2 >= PP_SLICE_MIN_K));
+  const PpPlan p = plan_pp(M, N, K, a_fmt, epi, a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || m->K2 >= PP_SLICE_MIN_K),
+                           wx);
   if (m->plans.size() > 4096) m->plans.clear();
   m->plans.emplace(key, p);
   return p;
@@ -722,7 +726,7 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
 #undef TVR_SK
     } else {
       PpPlan plan;
-      if (m && vec && epi != EPI_STATS) plan = plan_pp_cached(m, M, N, K, a_fmt, epi);
+      if (m && vec && epi != EPI_STATS) plan = plan_pp_cached(m, M, N, K, a_fmt, epi, a_fmt == ACT_X2F16 && W.x16);
       if (plan.sk_base >= 0) {
         if (plan.sk_base > 0)
           launch_pp(epi, Ah, lda, a_fmt, W, ldw, M, N, K, ep, acc_scale, 0, plan.sk_base, true, sl, st);
@@ -2489,13 +2493,14 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
 
 int tvr_gemm_plan(int32_t M, int32_t N, int32_t K, int32_t gemm_mode, int32_t flags, int32_t* out) {
   if (M <= 0 || N <= 0 || K <= 0 || !out || (gemm_mode != TVR_GEMM_X2F16 && gemm_mode != TVR_GEMM_BF16) ||
-      (flags & ~(TVR_PLAN_GELU | TVR_PLAN_MODEL_SLICED)))
+      (flags & ~(TVR_PLAN_GELU | TVR_PLAN_MODEL_SLICED | TVR_PLAN_EXACT16)))
     return fail(TVR_ERR_INVALID, "tvr_gemm_plan: bad argument");
   const int fmt = gemm_mode == TVR_GEMM_X2F16 ? ACT_X2F16 : ACT_BF16;
   if (K % (fmt == ACT_X2F16 ? 32 : 64) != 0) return fail(TVR_ERR_UNSUPPORTED, "tvr_gemm_plan: K not a k-tile multiple");
   // the same sliced rule as plan_pp_cached / launch_gemm
   const bool sliced = fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (flags & TVR_PLAN_MODEL_SLICED));
-  const PpPlan p = plan_pp(M, N, K, fmt, (flags & TVR_PLAN_GELU) ? EPI_SPLIT_GELU_ACT : EPI_RESID, sliced);
+  const PpPlan p = plan_pp(M, N, K, fmt, (flags & TVR_PLAN_GELU) ? EPI_SPLIT_GELU_ACT : EPI_RESID, sliced,
+                           fmt == ACT_X2F16 && (flags & TVR_PLAN_EXACT16));
   out[0] = p.ksplit;
   out[1] = p.tail_base;
   out[2] = p.tail_split;

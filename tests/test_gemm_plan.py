@@ -21,10 +21,11 @@ D, DMLP = 2560, 10240
 D1, K2 = 3 * D + DMLP, D + DMLP
 
 
-def plan(M, N, K, mode=X2F16, gelu=False, model_sliced=False):
+def plan(M, N, K, mode=X2F16, gelu=False, model_sliced=False, exact16=False):
     lib = tvr_amd._lib.load()
     out = (ctypes.c_int32 * 5)()
-    assert lib.tvr_gemm_plan(M, N, K, mode, (1 if gelu else 0) | (2 if model_sliced else 0), out) == 0
+    flags = (1 if gelu else 0) | (2 if model_sliced else 0) | (4 if exact16 else 0)
+    assert lib.tvr_gemm_plan(M, N, K, mode, flags, out) == 0
     return {"ksplit": out[0], "tail_base": out[1], "tail_split": out[2], "sk_base": out[3], "sk_blocks": out[4]}
 
 
@@ -41,12 +42,13 @@ def well_formed(p, M, N, K, bk=32):
     assert p["sk_base"] == -1 and p["sk_blocks"] == 0
 
 
+@pytest.mark.parametrize("exact16", [False, True])
 @pytest.mark.parametrize("l", range(32))
-def test_c2_layer_launches(l, monkeypatch):
+def test_c2_layer_launches(l, exact16, monkeypatch):
     monkeypatch.delenv("TVR_STREAM_K", raising=False)
     M = 156 + 52 * l
-    q = plan(M, D1, D, gelu=True)
-    o = plan(M, D, K2)
+    q = plan(M, D1, D, gelu=True, exact16=exact16)
+    o = plan(M, D, K2, exact16=exact16)
     well_formed(q, M, D1, D)
     well_formed(o, M, D, K2)
     # O + MLP-out: 10 column tiles per m-block -- never a plain launch on <= 70 of 256 CUs
@@ -80,7 +82,7 @@ def test_bad_arguments():
     assert lib.tvr_gemm_plan(0, D1, D, X2F16, 0, out) == tvr_amd._lib.TVR_ERR_INVALID
     assert lib.tvr_gemm_plan(16, D1, D, 0, 0, out) == tvr_amd._lib.TVR_ERR_INVALID  # f32 has no planar plan
     assert lib.tvr_gemm_plan(16, D1, 100, X2F16, 0, out) == tvr_amd._lib.TVR_ERR_UNSUPPORTED
-    assert lib.tvr_gemm_plan(16, D1, D, X2F16, 4, out) == tvr_amd._lib.TVR_ERR_INVALID  # unknown flag bit
+    assert lib.tvr_gemm_plan(16, D1, D, X2F16, 8, out) == tvr_amd._lib.TVR_ERR_INVALID  # unknown flag bit
     p = plan(300, 4096 * 3 + 16384, 4096, BF16, True)
     well_formed(p, 300, 4096 * 3 + 16384, 4096, bk=64)
 
