@@ -1419,6 +1419,7 @@ int32_t tvr_model_get_gemm(const tvr_model* m) { return m ? m->gemm_mode : -1; }
 // on the null stream
 static int replan_x2f16(tvr_model* m) {
   if (m->gemm_mode != TVR_GEMM_X2F16) return TVR_OK;
+  TVR_HIP(hipDeviceSynchronize());  // no launch on any stream may still read the planes about to be freed
   TVR_TRY(tvr_model_set_gemm(m, TVR_GEMM_F32, nullptr));
   return tvr_model_set_gemm(m, TVR_GEMM_X2F16, nullptr);
 }
