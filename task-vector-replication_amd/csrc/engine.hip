@@ -706,7 +706,11 @@ int launch_gemm(int epi, const void* A, int lda, int a_fmt, const MatW& W, int l
     const bool vec = planar_epilogue_vec(epi, ep, N);
     // x2f16 sliced accumulation (gemm_pingpong.hpp) on every GEMM of a model whose O + MLP-out K reaches
     // PP_SLICE_MIN_K (6.9B, 12B), or on any launch of that K
-    const bool sl = a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (m && m->K2 >= PP_SLICE_MIN_K));
+    // (one-plane weights, A/B of the precision it costs: TVR_WX_SLICE=0 runs them unsliced, 2 slices the
+    // O + MLP-out launches only)
+    static const int wx_slice = env_int("TVR_WX_SLICE", 1);
+    const bool sl = a_fmt == ACT_X2F16 && (K >= PP_SLICE_MIN_K || (m && m->K2 >= PP_SLICE_MIN_K)) &&
+                    (!W.x16 || wx_slice == 1 || (wx_slice == 2 && epi == EPI_RESID));
     if (ep.skinny && epi == EPI_BIAS && M <= SK_USE_M && !ep.out_rows && ep.k_split <= 1 && vec &&
         a_fmt != ACT_F16 && !W.x16 && !ep.a2) {
       // a few rows (the linearised entry's G on a rank of a head split): gemm_skinny.hpp
