@@ -320,6 +320,11 @@ def config_c2(model, mean, peak, reps=3):
         rate = len(task) * L / sec
         out[key] = {"ms_per_sweep": round(sec * 1e3, 3), "sites_per_s": round(rate, 1),
                     "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak, 4)}
+    out["peak_tflops"] = round(peak, 1)
+    if model.exact16 and model.gemm == "x2f16":
+        # the same work against the 3-product ceiling of rounds 1-4 (838.9 TF), for comparison across rounds
+        for key in ("accuracy", "dprob"):
+            out[key]["site_frac_vs_3product_ceiling"] = round(out[key]["site_tflops"] / PEAKS["x2f16"], 4)
     return out
 
 
