@@ -98,6 +98,12 @@ def test_processing_of_loaded_checkpoint(tmp_path, tiny):
     b = W.process_to_engine(cfg, {k: v.half().float() for k, v in sd.items()})
     for x, y in zip(a.tensors(), b.tensors()):
         assert torch.equal(x, y)
+    # a float16 checkpoint (every released Pythia) keeps its raw GEMM weights for the exact-fp16 GEMMs
+    assert a.raw16 is not None and a.raw16_unembed is not None
+    for ra, rb in zip(a.raw16, b.raw16):
+        assert torch.equal(ra.w1, rb.w1) and torch.equal(ra.w2, rb.w2) and torch.equal(ra.g1, rb.g1)
+    assert torch.equal(a.raw16_unembed[0], sd["embed_out.weight"].half())
+    assert W.process_to_engine(cfg, got, raw16=False).raw16 is None
 
 
 @pytest.mark.gpu
