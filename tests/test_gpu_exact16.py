@@ -13,7 +13,7 @@ subtracts it).  Checked here, on fp16-valued synthetic weights:
   tests/test_gpu_headline_shapes.py's fp32 bars (1e-4);
 * the exact-fp16 path against the processed-weight path of the same model
   (set_exact16(False)): clean logits, every CIE site, the extraction and the
-  trace's hook_resid_pre export agree to fp32 rounding (bar 1e-5 of max);
+  trace's hook_resid_pre export agree to fp32 rounding (bar 2e-5 of max; the CIE 5e-5);
 * the tiny model (d 64: the Q | K | V / MLP-in boundary inside a 256-column
   tile, two launches) the same way.
 """
@@ -28,13 +28,12 @@ import test_gpu_headline_shapes as H
 pytestmark = [pytest.mark.gpu]
 
 ARROW = tvr_amd.tasks.ARROW
-# exact16 vs the processed-weight path: fp32 rounding differences only (1e-5 of max); the CIE, a difference
-# of two probabilities, cancels: 5e-5 of max |CIE| (measured 2.1e-5 at the 2.8B width, where each path is
-# within the fp32 bar of 1e-4 of the oracle)
-X16_TOL = 1e-5
+# exact16 vs the processed-weight path: fp32 rounding differences of two exact rewrites only — 2e-5 of max
+# (measured <= 9.4e-6: logits 3.3e-6, extraction 7.0e-6, the centred trace export 8.1e-6 at the 12B width,
+# fused-statistics probabilities 9.4e-6); the CIE, a difference of two probabilities, cancels: 5e-5 of
+# max |CIE| (measured 1.3-2.7e-5; each path is within the fp32 bar of 1e-4 of the oracle)
+X16_TOL = 2e-5
 X16_TOL_CIE = 5e-5
-# probabilities through the fused-statistics unembed (2-product raw W_U against the 3-product processed one):
-# measured 9.4e-6 at the 2.8B width
 X16_TOL_PROB = 2e-5
 
 
