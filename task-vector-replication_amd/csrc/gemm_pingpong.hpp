@@ -105,10 +105,12 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_SLICE_FORM
 #define TVR_PP_SLICE_FORM 2
 #endif
-// The sliced form with one-plane weights (WX): 1 the scheduled pairs below (tile 0's two products, then
-// tile 1's, the previous pair's adds two per MFMA gap), 0 the compiler-placed generic loop.
+// The sliced form with one-plane weights (WX): 2 (default) the scheduled pairs below with the two tiles'
+// product chains interleaved (a1 w0 of tile 0, of tile 1, then a0 w0 of each), the previous pair's adds two
+// per MFMA gap: 592 / 601 TF on the probe's shapes; 1 tile 0's chain then tile 1's (each chain's second MFMA
+// right behind its first: 577 / 587, profiles/r05/slice_form_wx2_ab_r05as.txt); 0 the compiler-placed loop.
 #ifndef TVR_PP_SLICE_FORM_WX
-#define TVR_PP_SLICE_FORM_WX 1
+#define TVR_PP_SLICE_FORM_WX 2
 #endif
 // One-plane weights: 1 stage the 2-piece activation regions in the read-light phases (pp_tile), 0 (default)
 // the 3-product order.  Measured within noise (qkv / o probe shapes 654 / 672 vs 651 / 671 TF, sliced 578 /
@@ -438,19 +440,20 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   // phase's cluster (tc, for acc[ci][cj + 0..1]) and added there, while its first MFMAs run
   [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mfma_quadrant = [&](int i0, int j0, const frag (&fw)[2][2], auto part, int ci, int cj) {
-#if TVR_PP_SLICE_FORM_WX == 1
+#if TVR_PP_SLICE_FORM_WX >= 1
     if constexpr (FMT == ACT_X2F16 && SL && WX && !decltype(part)::value) {
-      // sliced, one-plane weights: per tile pair (i, 0..1) the tile-0 slice (a1 w0, then a0 w0 on it), then
-      // tile 1's, two of the previous pair's 8 slice-sum adds after each MFMA: the tile-0 sums a pair reads
-      // were finished 3 MFMAs before its first add, the tile-1 sums 3 before theirs (>= 9 issue slots: no
-      // s_nop before a read of an MFMA result); the last pair carried into the next phase (tc), as form 2
+      // sliced, one-plane weights: per tile pair (i, 0..1) the two slices' products (form 2: a1 w0 of both
+      // tiles, then a0 w0 of both; form 1: tile 0's chain, then tile 1's), two of the previous pair's 8
+      // slice-sum adds after each MFMA (tile 0's sums first); the last pair carried into the next phase (tc),
+      // as the 3-product form 2
       f32x4 t[4][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int di = i == 0 ? ci : i0 + i - 1, dj = i == 0 ? cj : j0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int j = q >> 1, pz = q & 1;  // MFMA q: product pz of tile j (0: a1 w0, 1: a0 w0)
+          // MFMA q: product pz of tile j (0: a1 w0, 1: a0 w0); form 2 interleaves the two tiles' chains
+          const int j = TVR_PP_SLICE_FORM_WX == 2 ? (q & 1) : (q >> 1), pz = TVR_PP_SLICE_FORM_WX == 2 ? (q >> 1) : (q & 1);
           t[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][pz == 0 ? 1 : 0],
                                                              pz == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : t[i][j], 0, 0, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -697,7 +700,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   if (vi == 8) {
     kloop(std::integral_constant<bool, false>{});
 #if TVR_PP_SLICE_FORM >= 1
-    if constexpr (FMT == ACT_X2F16 && SL && (!WX || TVR_PP_SLICE_FORM_WX == 1)) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
+    if constexpr (FMT == ACT_X2F16 && SL && (!WX || TVR_PP_SLICE_FORM_WX >= 1)) {  // the last cluster's carried pair (q4: tiles (7, 0..1))
       acc[7][0] = slice_add(acc[7][0], tc[0]);
       acc[7][1] = slice_add(acc[7][1], tc[1]);
     }
