@@ -7,7 +7,6 @@ distributed.py, with the oracle standing in for each rank's GPU sweep.
   division by the global count) == the unsharded mean.
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -15,15 +14,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store_file, q):
+    # a file rendezvous: no port to race for with other processes on the machine
+    dist.init_process_group("gloo", init_method=f"file://{store_file}", rank=rank, world_size=world)
     try:
         import tvr_amd
         from tvr_amd import distributed as D
@@ -60,11 +53,11 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_sharded_sweeps_match_single_process(world):
+def test_sharded_sweeps_match_single_process(world, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    store = tmp_path / "gloo_store"
+    procs = [ctx.Process(target=_worker, args=(r, world, str(store), q)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
@@ -161,9 +154,8 @@ class OracleEngine:
         return self._outs(logits, [int(s["target"]) for s in sites] if want_prob else None, topk)
 
 
-def _site_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _site_worker(rank, world, store_file, q):
+    dist.init_process_group("gloo", init_method=f"file://{store_file}", rank=rank, world_size=world)
     try:
         from tvr_amd import distributed as D
         out = _site_sweeps(dist.group.WORLD)
@@ -200,15 +192,15 @@ def _site_sweeps(group):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_site_sharded_injection_sweeps_match_single_process(world):
+def test_site_sharded_injection_sweeps_match_single_process(world, tmp_path):
     """The layer sweeps (a4 accuracy, a5 Δprob) and the per-layer FV top-k
     accuracy with (prompt, layer) sites round-robin over gloo ranks + one
     all_gather == the same experiment code in one process == the reference
     loop restated by the oracle."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=_site_worker, args=(r, world, port, q)) for r in range(world)]
+    store = tmp_path / "gloo_store"
+    procs = [ctx.Process(target=_site_worker, args=(r, world, str(store), q)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
