@@ -118,6 +118,14 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_WX_STAGE
 #define TVR_PP_WX_STAGE 0
 #endif
+// One-plane weights: the wide wave tile (pp_tile_wt: 4 x 2 waves of 64 x 128, balanced read segments) —
+// 2 (default) two phases per k-tile when unsliced, 1 four phases, 0 pp_tile's 2 x 4 waves of 128 x 64.
+// Probe, one box, 3 interleaved rounds (profiles/r06/wide_tile_probe_r06c.txt): qkv / o shapes 641 / 655 TF
+// (pp_tile) -> 651 / 661 (wide) -> 661 / 663 (wide, two phases); sliced 577 / 584 -> 601 / 610 (wide); PMC:
+// MFMA busy 73.7 -> 77.2 -> 78.3 % at 1.69 -> 1.63 -> 1.62 GHz (the power cap gives back most of the cycles)
+#ifndef TVR_PP_WX_WIDE
+#define TVR_PP_WX_WIDE 2
+#endif
 // One-plane weights, unsliced: 1 the two-phase, three-buffer K loop (pp_tile P2), 0 the four-phase one
 #ifndef TVR_PP_WX_2PHASE
 #define TVR_PP_WX_2PHASE 0
@@ -175,10 +183,14 @@ __device__ __forceinline__ void pp_stats_rows(const GemmEpi& ep, const float* L,
   }
 }
 
-template <int EPI, int FMT, bool NOSTORE = false>
-__device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (&acc)[8][4], float* L, int row0,
+// TM x TN accumulators per wave: 8 x 4 (waves 2 rows x 4 columns of 128 x 64) or 4 x 8 (the wide-tile
+// one-plane form, pp_tile_wt: waves 4 rows x 2 columns of 64 x 128); half p of the tile (rows 128 p ..)
+// comes from the waves whose rows lie in it
+template <int EPI, int FMT, bool NOSTORE = false, int TM = 8, int TN = 4>
+__device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (&acc)[TM][TN], float* L, int row0,
                                                 int col0, int Mlim, int Nlim, int wr, int wc, int lane, int t,
                                                 float acc_scale) {
+  static_assert((TM == 8 && TN == 4) || (TM == 4 && TN == 8), "wave tile 128 x 64 or 64 x 128");
   // A thread's columns are the same in every row it stores (the row step, 512
   // threads, is a multiple of the threads per row), so the bias is loaded once
   // before the row loops: no global load inside them, only LDS reads and stores.
@@ -197,12 +209,13 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
   }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    if (wr == p) {
+    if ((TM == 8 ? wr : wr >> 1) == p) {
+      const int r0 = TM == 8 ? 0 : (wr & 1) * 64;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *(f32x4*)(L + (i * 16 + (lane & 15)) * PP_EPI_LDR + wc * 64 + j * 16 + 4 * (lane >> 4)) =
+        for (int j = 0; j < TN; ++j)
+          *(f32x4*)(L + (r0 + i * 16 + (lane & 15)) * PP_EPI_LDR + wc * (16 * TN) + j * 16 + 4 * (lane >> 4)) =
               acc[i][j] * acc_scale;
     }
     __syncthreads();
@@ -764,6 +777,338 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   }
 }
 
+// The one-plane (WX) tile on a WIDE wave tile: 8 waves as 4 (rows, wr) x 2 (columns, wc) of 64 x 128 each
+// (acc[4][8]) instead of 2 x 4 of 128 x 64.  With two activation planes and one weight plane a wave's
+// fragment reads per k-tile are (rows / 16) x 2 + columns / 16: 16 here against 20 (8 x 2 + 4), and the
+// four phases' read segments are balanced — 4 fragments each — by reading the NEXT k-tile's first two row
+// tiles in q4, whose cluster needs nothing read in its own segment:
+//     q1  rows 0-31 x cols 0-63     reads W_lo(t)    stages A_hi(t+1)   (2 pieces per wave)
+//     q2  rows 0-31 x cols 64-127   reads W_hi(t)    stages A_lo(t+2)   (2)
+//     q3  rows 32-63 x cols 64-127  reads A_hi(t)    stages W_lo(t+2)   (1)
+//     q4  rows 32-63 x cols 0-63    reads A_lo(t+1)  stages W_hi(t+2)   (1)
+// (pp_tile's q1 reads 10 fragments + 2 pieces and q3 8 + 2, longer than the partner's 16-MFMA cluster;
+// q2 and q4 2 and 0.)  Regions: A_lo / A_hi = rows 0-31 / 32-63 of every wave row's 64 (2 planes, 16 KB),
+// W_lo / W_hi = columns 0-63 / 64-127 of every wave column's 128 (8 KB).  Every region is restaged 2 phases
+// after its last read, issued 6 phases before its first read and retired one phase before it by
+// vmcnt(6) (the pieces issued since: 1 + 2 + 2 + 1 in every phase), as pp_tile's rules.  Per output
+// element the MFMA sequence is pp_tile's (a1 w0, then a0 w0, k-slice by k-slice; sliced: the slice's sum
+// added once): bit-identical results.  A/B: TVR_PP_WX_WIDE=0, or VAR 16 / 17 (probe).
+#ifndef TVR_WT_SGB
+#define TVR_WT_SGB 1
+#endif
+template <int EPI, bool VEC, int VAR, bool SL, bool TWO = false>
+__device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int lda, size_t aps,
+                                           const uint16_t* __restrict__ W, int ldw, float acc_scale, int M, int N,
+                                           const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part,
+                                           int has_part, unsigned long long st0, unsigned long long sr0) {
+  using F = PlanarFmt<ACT_X2F16>;
+  using frag = typename F::frag;
+  constexpr int BK = F::BK;            // 32 halves: 64 B per plane row
+  constexpr int CPR = BK / 8;          // 4 chunks of 16 B per row
+  constexpr int RPP = 64 / CPR;        // 16 rows per 1 KB piece
+  constexpr int PPP = 128 / RPP;       // 8 pieces per plane per region
+  constexpr int PL = 256 * BK;         // halves per plane per buffer
+  constexpr int BUF = 3 * PL;          // A hi / lo planes + one weight plane
+  constexpr int NBUF = TWO ? 3 : 2;    // TWO: the two-phase loop's three buffers (below)
+  constexpr int DUMMY = NBUF * BUF;
+  constexpr int LDS_HALVES = (NBUF * BUF + 512) > PP_EPI_LDS ? (NBUF * BUF + 512) : PP_EPI_LDS;
+  static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_HALVES];
+
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  const int wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const uint16_t* Ab = ep.a2 != nullptr && n0 >= ep.a2_col ? ep.a2 : A;
+
+  // staging map: region R (0 A_lo, 1 A_hi, 2 W_lo, 3 W_hi); A regions 2 pieces per wave, W regions 1
+  const uint16_t* src[4][2];
+  int dst[4][2];
+#pragma unroll
+  for (int R = 0; R < 4; ++R) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int pi = R >= 2 ? wave_s : 2 * wave_s + s;
+      const int plane = pi / PPP, x0 = (pi % PPP) * RPP;  // region row of the piece's first row
+      const int trow0 = R < 2 ? ((x0 >> 5) << 6) + (x0 & 31) + 32 * R : ((x0 >> 6) << 7) + (x0 & 63) + 64 * (R - 2);
+      const int row = trow0 + lane / CPR;
+      const int chunk = (lane % CPR) ^ planar_g<CPR>(row);
+      if (R < 2) {
+        const int am = min(m0 + row, M - 1);
+        src[R][s] = Ab + plane * aps + (size_t)(ep.a_rows ? ep.a_rows[am] : am) * lda + chunk * 8;
+        dst[R][s] = plane * PL + trow0 * BK;
+      } else {
+        src[R][s] = W + (size_t)min(n0 + row, N - 1) * ldw + chunk * 8;
+        dst[R][s] = 2 * PL + trow0 * BK;
+      }
+    }
+  }
+  auto stage = [&](int R, int kt) {
+    const bool live = kt < nk;
+    const int koff = live ? (kbeg + kt) * BK : 0;
+    const int boff = (TWO ? kt % 3 : kt & 1) * BUF;
+#pragma unroll
+    for (int s = 0; s < (R >= 2 ? 1 : 2); ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
+  };
+
+  // fragment offsets: plane f of the wave's first row tile / the weight plane at its first column tile
+  int aoff[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int ra = wr * 64 + (lane & 15), c = lane >> 4;
+    aoff[f] = f * PL + ra * BK + ((c ^ planar_g<CPR>(ra)) << 3);
+  }
+  const int rb = wc * 128 + (lane & 15);
+  const int woff = 2 * PL + rb * BK + (((lane >> 4) ^ planar_g<CPR>(rb)) << 3);
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+  frag fa[4][2], fw[8];
+
+  // live 16-row slices of the wave's 64 rows (rows past M are copies of row M - 1): the PART loop skips the
+  // padding slices' fragment reads and MFMAs (staging and barriers stay)
+  const int vi = __builtin_amdgcn_readfirstlane(min(4, max(0, (M - m0 - wr * 64 + 15) >> 4)));
+  auto read_a = [&](const uint16_t* base, int i0, auto part) {
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+      if (!decltype(part)::value || i < vi)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) fa[i][f] = *(const frag*)(base + aoff[f] + i * 16 * BK);
+  };
+  auto read_w = [&](const uint16_t* base, int j0, auto part) {
+    if (decltype(part)::value && vi == 0) return;
+#pragma unroll
+    for (int j = j0; j < j0 + 4; ++j) fw[j] = *(const frag*)(base + woff + j * 16 * BK);
+  };
+  [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  // one phase's cluster: row tiles i0, i0 + 1 x column tiles j0 .. j0 + NJ - 1 (4, or 8 in the two-phase
+  // loop), two products each
+  constexpr int NJ = TWO ? 8 : 4, NP = NJ / 2;  // column tiles, tile pairs per row
+  auto cluster = [&](int i0, int j0, auto part, int ci, int cj) {
+    if constexpr (SL && !decltype(part)::value) {
+      // sliced: tile pairs (i, j..j+1) in turn, the two tiles' chains interleaved (a1 w0 of both, then a0 w0
+      // of both), two of the previous pair's 8 slice-sum adds after each MFMA; the cluster's last pair is
+      // carried into the next phase (tc) — pp_tile's form 2
+      f32x4 s[2][2];  // pair q's slice sums in s[q & 1] (the previous pair's are added while it runs)
+#pragma unroll
+      for (int q = 0; q < 2 * NP; ++q) {
+        const int i = i0 + q / NP, j = j0 + 2 * (q % NP);  // pair q: tiles (i, j), (i, j + 1)
+        const int pi = q == 0 ? ci : i0 + (q - 1) / NP, pj = q == 0 ? cj : j0 + 2 * ((q - 1) % NP);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int jj = u & 1, pz = u >> 1;  // MFMA u: product pz (0: a1 w0, 1: a0 w0) of tile (i, j + jj)
+          s[q & 1][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j + jj], fa[i][pz == 0 ? 1 : 0],
+                                                                 pz == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : s[q & 1][jj],
+                                                                 0, 0, 0);
+          if (TVR_WT_SGB) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+          for (int e = 2 * u; e < 2 * u + 2; ++e)
+            acc[pi][pj + (e >> 2)][e & 3] += q == 0 ? tc[e >> 2][e & 3] : s[(q - 1) & 1][e >> 2][e & 3];
+          if (TVR_WT_SGB) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        if (NP == 4 && q == NP - 1) __builtin_amdgcn_sched_barrier(0);  // two-phase: schedule each row's pairs apart
+      }
+      tc[0] = s[(2 * NP - 1) & 1][0];
+      tc[1] = s[(2 * NP - 1) & 1][1];
+      return;
+    }
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i)
+#pragma unroll
+      for (int j = j0; j < j0 + NJ; ++j) {
+        if (decltype(part)::value && i >= vi) continue;
+        f32x4 c = acc[i][j];
+        if constexpr (SL) {
+          f32x4 s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][0], s, 0, 0, 0);
+          c = slice_add(c, s);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][0], c, 0, 0, 0);
+        }
+        acc[i][j] = c;
+      }
+  };
+  constexpr bool prio = !SL;
+#define TVR_PP_CLUSTER(...)                  \
+  __builtin_amdgcn_s_barrier();              \
+  __builtin_amdgcn_sched_barrier(0);         \
+  if (prio) __builtin_amdgcn_s_setprio(1);   \
+  __VA_ARGS__;                               \
+  if (prio) __builtin_amdgcn_s_setprio(0);   \
+  __builtin_amdgcn_sched_barrier(0);         \
+  __builtin_amdgcn_s_barrier();              \
+  __builtin_amdgcn_sched_barrier(0)
+
+  // prologue, the loop's stage history.  Four phases: A_lo(0) W_lo(0) W_hi(0) A_hi(0) A_lo(1) W_lo(1) W_hi(1),
+  // retire A_lo(0) / W_lo(0) (7 pieces issued after them).  Two phases: A_lo W_lo A_hi W_hi of k-tiles 0 and
+  // 1, retire k-tile 0 (6 pieces after W_hi(0)).  Then read A_lo(0): the last phase's read of k-tile -1
+  if constexpr (TWO) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      stage(0, k);
+      stage(2, k);
+      stage(1, k);
+      stage(3, k);
+    }
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    stage(0, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(0, 1);
+    stage(2, 1);
+    stage(3, 1);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (vi == 4)
+    read_a(lds, 0, std::integral_constant<bool, false>{});
+  else
+    read_a(lds, 0, std::integral_constant<bool, true>{});
+  if (wr >= 2) {  // the group offset: waves 4-7 run one barrier behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  unsigned long long d_loop0 = 0, d_loop1 = 0;
+  if constexpr (VAR == 6 || VAR == 8) d_loop0 = __builtin_amdgcn_s_memtime();
+  auto kloop = [&](auto part) {
+    if constexpr (TWO) {
+      // Two phases per k-tile, 32 MFMAs each, three LDS buffers (k-tile t in buffer t % 3):
+      //   P1  rows 0-31 x all 128 cols   reads W_lo, W_hi(t)          stages A_lo(t+2), W_lo(t+2)  (3 pieces)
+      //   P2  rows 32-63 x all 128 cols  reads A_hi(t), A_lo(t+1)     stages A_hi(t+2), W_hi(t+2)  (3 pieces)
+      // Each region is restaged >= 2 phases after its last read (buffer t % 3 held k-tile t - 1... t - 3's
+      // regions, last read >= 2 phases before) and retired one phase before its first read, >= 2 phases (of
+      // ~512 MFMA cycles) after its issue: vmcnt(4) in P1 (A_lo(t+1), A_hi(t): 4 pieces issued after
+      // A_lo(t+1)), vmcnt(3) in P2 (W_hi(t+1): 3 after it)
+      for (int kt = 0; kt < nk; ++kt) {
+        const uint16_t* cur = lds + (kt % 3) * BUF;
+        read_w(cur, 0, part);
+        read_w(cur, 4, part);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A_lo(kt+1) (P1 of kt-1), A_hi(kt): read in P2
+        stage(0, kt + 2);
+        stage(2, kt + 2);
+        TVR_PP_CLUSTER(cluster(0, 0, part, 3, 6));  // the previous cluster's carried pair: tiles (3, 6..7)
+        read_a(cur, 2, part);
+        read_a(lds + ((kt + 1) % 3) * BUF, 0, part);
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // W_hi(kt+1) (P2 of kt-1), W_lo(kt+1): read in P1
+        stage(1, kt + 2);
+        stage(3, kt + 2);
+        TVR_PP_CLUSTER(cluster(2, 0, part, 1, 6));
+      }
+      return;
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint16_t* cur = lds + (kt & 1) * BUF;
+      // q1: rows 0-31 x cols 0-63
+      read_w(cur, 0, part);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // W_hi(kt) (q4 of kt-2), read in q2
+      stage(1, kt + 1);
+      TVR_PP_CLUSTER(cluster(0, 0, part, 3, 2));  // (ci, cj): the previous phase's carried pair (q4: tiles (3, 2..3))
+      // q2: rows 0-31 x cols 64-127
+      read_w(cur, 4, part);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+      stage(0, kt + 2);
+      TVR_PP_CLUSTER(cluster(0, 4, part, 1, 2));
+      // q3: rows 32-63 x cols 64-127
+      read_a(cur, 2, part);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1) (q2 of kt-1), read in q4
+      stage(2, kt + 2);
+      TVR_PP_CLUSTER(cluster(2, 4, part, 1, 6));
+      // q4: rows 32-63 x cols 0-63; reads the next k-tile's A_lo (its cluster needs nothing read here)
+      read_a(lds + ((kt + 1) & 1) * BUF, 0, part);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // W_lo(kt+1) (q3 of kt-1), read in q1
+      stage(3, kt + 2);
+      TVR_PP_CLUSTER(cluster(2, 0, part, 3, 6));
+    }
+  };
+  if (vi == 4) {
+    kloop(std::integral_constant<bool, false>{});
+    if constexpr (SL) {  // the last cluster's carried pair (q4: tiles (3, 2..3); two-phase: (3, 6..7))
+      acc[3][TWO ? 6 : 2] = slice_add(acc[3][TWO ? 6 : 2], tc[0]);
+      acc[3][TWO ? 7 : 3] = slice_add(acc[3][TWO ? 7 : 3], tc[1]);
+    }
+  } else {
+    kloop(std::integral_constant<bool, true>{});
+  }
+#undef TVR_PP_CLUSTER
+  if constexpr (VAR == 6 || VAR == 8) d_loop1 = __builtin_amdgcn_s_memtime();
+  if (wr < 2) __builtin_amdgcn_s_barrier();  // balance the group offset
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if constexpr (VEC) {
+    __syncthreads();
+    float* L = reinterpret_cast<float*>(lds);
+    if (has_part) {
+      GemmEpi pe = ep;
+      pe.out0 = part;
+      pe.ld0 = 256;
+      pe.out_rows = nullptr;
+      pp_epilogue_lds<EPI, ACT_X2F16, VAR == 8, 4, 8>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+    } else {
+      pp_epilogue_lds<EPI, ACT_X2F16, VAR == 8, 4, 8>(ep, acc, L, m0, n0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+    }
+    if ((VAR == 6 || VAR == 8) && ep.stamps && t == 0) {
+      unsigned long long* o = ep.stamps + 4 * blockIdx.x;
+      o[0] = st0;
+      o[1] = d_loop0;
+      o[2] = d_loop1;
+      o[3] = __builtin_amdgcn_s_memtime();
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_STATS) {
+    return;
+  } else {
+    if (acc_scale != 1.0f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] *= acc_scale;
+    }
+    if (has_part) {
+      GemmEpi pe = ep;
+      pe.out0 = part;
+      pe.ld0 = 256;
+      gemm_epilogue16t<EPI, ACT_X2F16, VEC, 4, 8>(pe, acc, M - m0, N - n0, wr * 64, wc * 128, lane);
+    } else {
+      gemm_epilogue16t<EPI, ACT_X2F16, VEC, 4, 8>(ep, acc, M, N, m0 + wr * 64, n0 + wc * 128, lane);
+    }
+    if (ep.stamps && t == 0) {
+      ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
+      ep.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - sr0;
+    }
+  }
+}
+
+// One tile of a launch: the wide-tile form for one-plane weights (TVR_PP_WX_WIDE 1: four phases, 2: two;
+// VAR 16 / 20 force the four / two-phase wide tile, 17 pp_tile), else pp_tile
+template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX>
+__device__ __forceinline__ void pp_tile_any(const uint16_t* __restrict__ A, int lda, size_t aps,
+                                            const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale,
+                                            int M, int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk,
+                                            float* part, int has_part, unsigned long long st0,
+                                            unsigned long long sr0) {
+  constexpr bool wide = WX && FMT == ACT_X2F16 &&
+                        (VAR == 16 || VAR == 20 || (VAR != 17 && TVR_PP_WX_WIDE && (VAR == 0 || VAR == 6 || VAR == 8)));
+  // (the sliced form stays on four phases: the two-phase cluster keeps all 8 weight fragments live through
+  // both clusters, 16 VGPRs more than the 252 the sliced four-phase form holds — it spilled 38)
+  constexpr bool two = VAR == 20 || (VAR != 16 && TVR_PP_WX_WIDE == 2 && !SL);
+  constexpr int V = (VAR == 16 || VAR == 17 || VAR == 20) ? 0 : VAR;
+  if constexpr (wide)
+    pp_tile_wt<EPI, VEC, V, SL, two>(A, lda, aps, W, ldw, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part, st0,
+                                     sr0);
+  else
+    pp_tile<EPI, FMT, VEC, V, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part,
+                                      st0, sr0);
+}
+
 // K must be a multiple of BK (host-checked); any M, N.
 // VAR (diagnostic builds, tools/gemm_split_probe): 1 no staging in the loop
 // (stale LDS: timing only), 2 no s_setprio, 13 s_setprio 1 once for waves 4-7, 14 the cluster flips in the
@@ -772,7 +1117,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 // start, loop end, end) of wave 0 to ep.stamps[4 block + i], 7 the register
 // epilogue (no LDS pass), 8 the stamps of 6 with the epilogue's global stores
 // skipped (timing only), 12 every k-tile staged from k-tile 0 (L2-hot operands,
-// same instruction stream: timing only).  SKM: the stream-K form (sk_blocks
+// same instruction stream: timing only), 16 / 17 the one-plane wide / narrow wave tile.  SKM: the stream-K form (sk_blocks
 // blocks; EPI_BIAS partial tiles only).  SL: x2f16 sliced accumulation (above).  WX: x2f16 activations
 // against weights exact in fp16 (one plane staged, two products; pp_tile).
 template <int EPI, int FMT, bool VEC = true, int VAR = 0, bool SKM = false, bool SL = false, bool WX = false>
@@ -810,7 +1155,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       const int nk = (int)min((long long)(nk_all - kbeg), it1 - it);
       int m0, n0;
       pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-      pp_tile<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+      pp_tile_any<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                   ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, 1, st0, sr0);
       it += nk;
     };
@@ -826,7 +1171,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
     const int kbeg = (int)((long long)split * nk_all / S);
     const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
-    pp_tile<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+    pp_tile_any<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                 ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS, S > 1, st0, sr0);
   }
 }

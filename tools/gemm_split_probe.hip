@@ -166,6 +166,19 @@ int main(int argc, char** argv) {
                                      : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true, true>;
           hipLaunchKernelGGL(kw, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2ppwxw" || path == "x2ppwxn" || path == "x2ppslwxw" || path == "x2ppslwxn" ||
+                   path == "x2ppwxw2" || path == "x2ppslwxw2") {
+          // one-plane weights on the wide (4 x 2 waves of 64 x 128, VAR 16; two-phase VAR 20) / narrow (pp_tile,
+          // VAR 17) wave tile
+          grid = gemm_pingpong_grid(s.M, s.N);
+          auto kw = path == "x2ppwxw"   ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 16, false, false, true>
+                    : path == "x2ppwxn" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 17, false, false, true>
+                    : path == "x2ppwxw2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 20, false, false, true>
+                    : path == "x2ppslwxw2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 20, false, true, true>
+                    : path == "x2ppslwxw" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 16, false, true, true>
+                                          : gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 17, false, true, true>;
+          hipLaunchKernelGGL(kw, dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
         } else if (path == "x2ppsl" || path == "x2ppsl14" || path == "x2ppsl13") {  // sliced accumulation (6.9B / 12B)
           grid = gemm_pingpong_grid(s.M, s.N);
           auto ks = path == "x2ppsl" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 0, false, true>
