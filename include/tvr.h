@@ -197,7 +197,8 @@ int tvr_trace_destroy(tvr_trace* trace);
 int tvr_trace_flush(tvr_trace* trace, void* stream);
 /* Copy a traced hook into a caller device buffer [n_tokens][d] (async on
  * `stream`): what = TVR_TRACE_RESID_PRE gives blocks.{layer}.hook_resid_pre
- * (layer == n_layers: the final residual), TVR_TRACE_Z blocks.{layer}.attn.hook_z. */
+ * (layer == n_layers: the final residual), TVR_TRACE_Z blocks.{layer}.attn.hook_z.
+ * dst needs only float alignment (4 B). */
 enum tvr_trace_hook { TVR_TRACE_RESID_PRE = 0, TVR_TRACE_Z = 1 };
 int tvr_trace_read(const tvr_trace* trace, int32_t what, int32_t layer, float* dst,
                    void* stream);

@@ -79,6 +79,7 @@ ABI_VERSION = 11  # include/tvr.h TVR_ABI_VERSION
 
 # include/tvr.h enum tvr_gemm_mode
 GEMM_MODES = {"f32": 0, "x3bf16": 1, "x2f16": 2, "bf16": 3}
+GEMM_NAMES = {v: k for k, v in GEMM_MODES.items()}
 
 SIGNATURES = {
     "tvr_version": (ctypes.c_char_p, []),
@@ -151,6 +152,12 @@ class EngineError(RuntimeError):
     pass
 
 
+class RangeError(EngineError):
+    """TVR_ERR_RANGE: an x2f16 GEMM input left the fp16 split's range (the
+    results since the last check are not fp32-accurate).  The experiment
+    functions retry on a path without that limit (``Model.range_fallback``)."""
+
+
 def load(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     """Load libtvr.so (cached).  Raises if it is missing: build it with
     ``python __graft_entry__.py`` or ``make -C task-vector-replication_amd/csrc``."""
@@ -196,6 +203,8 @@ def check(rc: int, what: str) -> None:
     msg = (load().tvr_last_error() or b"").decode(errors="replace")
     if rc == TVR_ERR_INVALID:
         raise ValueError(f"{what}: {msg}")
+    if rc == TVR_ERR_RANGE:
+        raise RangeError(f"{what} failed ({rc}): {msg}")
     raise EngineError(f"{what} failed ({rc}): {msg}")
 
 

@@ -1727,8 +1727,14 @@ int tvr_trace_read(const tvr_trace* t, int32_t what, int32_t layer, float* dst, 
   if (what == TVR_TRACE_RESID_PRE && t->uncentred && t->n_tokens > 0) {
     // TL's residual stream is centred (every write to it is: W_E, W_O, W_out, their biases); the x16 path's
     // differs from it by one constant per row
-    hipLaunchKernelGGL(center_rows_kernel, dim3((t->n_tokens + 3) / 4), dim3(256), 0, (hipStream_t)stream, src, dst,
-                       t->n_tokens, d);
+    // (a caller's dst may be any float*, e.g. an offset view: the float4 form only where it is 16-B aligned)
+    const bool v4 = ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && d % 4 == 0;
+    if (v4)
+      hipLaunchKernelGGL(center_rows_kernel<true>, dim3((t->n_tokens + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                         src, dst, t->n_tokens, d);
+    else
+      hipLaunchKernelGGL(center_rows_kernel<false>, dim3((t->n_tokens + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                         src, dst, t->n_tokens, d);
     TVR_HIP(hipGetLastError());
     return TVR_OK;
   }

@@ -64,21 +64,31 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
 
 // dst[r] = src[r] - mean(src[r]) (one wave per row, d % 4 == 0): the exact-fp16 weight path's residual
 // stream carries one extra constant per row (engine.hip tvr_model, x16), which the TL residual lacks
+// V4: src and dst 16-B aligned, d % 4 == 0 (float4 accesses); else element-wise (a caller's offset view)
+template <bool V4>
 __global__ void center_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int d) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;
-  const float4* x = (const float4*)(src + (size_t)r * d);
-  float4* y = (float4*)(dst + (size_t)r * d);
   float s = 0.f;
-  for (int c = lane; c < d / 4; c += 64) {
-    const float4 v = x[c];
-    s += (v.x + v.y) + (v.z + v.w);
-  }
-  const float mean = wave_sum(s) / (float)d;
-  for (int c = lane; c < d / 4; c += 64) {
-    const float4 v = x[c];
-    y[c] = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  if constexpr (V4) {
+    const float4* x = (const float4*)(src + (size_t)r * d);
+    float4* y = (float4*)(dst + (size_t)r * d);
+    for (int c = lane; c < d / 4; c += 64) {
+      const float4 v = x[c];
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    const float mean = wave_sum(s) / (float)d;
+    for (int c = lane; c < d / 4; c += 64) {
+      const float4 v = x[c];
+      y[c] = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+    }
+  } else {
+    const float* x = src + (size_t)r * d;
+    float* y = dst + (size_t)r * d;
+    for (int c = lane; c < d; c += 64) s += x[c];
+    const float mean = wave_sum(s) / (float)d;
+    for (int c = lane; c < d; c += 64) y[c] = x[c] - mean;
   }
 }
 

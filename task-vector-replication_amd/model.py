@@ -25,6 +25,8 @@ import contextlib
 import ctypes
 import functools
 import inspect
+import random
+import warnings
 import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
@@ -44,7 +46,17 @@ SITE_DTYPE = np.dtype([(f, np.int32) for f in _lib.SITE_FIELDS])
 def range_checked(fn):
     """Run ``fn`` (an experiment function taking ``model``) inside the model's
     range scope: the x2f16 range flag is read once when the outermost scope
-    ends instead of after every engine call."""
+    ends instead of after every engine call.
+
+    If that check fails (``_lib.RangeError``: a GEMM input reached the fp16
+    split's limit, so the call's results are not fp32-accurate), the model
+    moves to the next path without that limit (``Model.range_fallback``:
+    the processed-weight GEMMs when the exact-fp16 ones were bound — their A
+    operand is LNPre(x)·γ — else gemm ``"x3bf16"``), warns, records it in
+    ``model.range_fallbacks``, restores the global ``random`` state the call
+    started from and runs the call again: same process, same prompts (the
+    functions shuffle private copies of their inputs; substitute_task's
+    in-place sort is idempotent)."""
     sig = inspect.signature(fn)
 
     @functools.wraps(fn)
@@ -55,8 +67,18 @@ def range_checked(fn):
             model = None
         if not isinstance(model, Model):
             return fn(*args, **kwargs)
-        with model.range_scope(fn.__name__):
-            return fn(*args, **kwargs)
+        if model._range_depth > 0 or not model.range_fallback:  # the outermost call retries
+            with model.range_scope(fn.__name__):
+                return fn(*args, **kwargs)
+        state = random.getstate()
+        while True:
+            try:
+                with model.range_scope(fn.__name__):
+                    return fn(*args, **kwargs)
+            except _lib.RangeError as e:
+                if not model._fall_back(fn.__name__, e):
+                    raise
+                random.setstate(state)
     return wrapper
 
 
@@ -182,6 +204,10 @@ class Model(TokenizerMixin):
         self.exact16 = False
         self._x16_c = None
         self.gemm = "f32"
+        # what an experiment function does when the x2f16 range check fails (range_checked): retry on the
+        # next path without the limit (True), or raise (False); the fallbacks taken, as (function, path)
+        self.range_fallback = True
+        self.range_fallbacks: List[tuple] = []
         if weights.raw16 is not None:  # bound first: the x2f16 planes are then built without W2's
             self.set_exact16(True)
         self.set_gemm(gemm)
@@ -239,9 +265,11 @@ class Model(TokenizerMixin):
         if mode not in _lib.GEMM_MODES:
             raise ValueError(f"gemm mode must be one of {sorted(_lib.GEMM_MODES)}, got {mode!r}")
         with torch.cuda.device(self.device):
-            _lib.check(self._lib.tvr_model_set_gemm(self._h, _lib.GEMM_MODES[mode], self._stream()),
-                       "tvr_model_set_gemm")
-        self.gemm = mode
+            try:
+                _lib.check(self._lib.tvr_model_set_gemm(self._h, _lib.GEMM_MODES[mode], self._stream()),
+                           "tvr_model_set_gemm")
+            finally:  # a failed switch leaves the engine in the fp32 mode: mirror it
+                self.gemm = _lib.GEMM_NAMES.get(self._lib.tvr_model_get_gemm(self._h), mode)
 
     def set_exact16(self, on: bool) -> None:
         """Bind (or detach) the checkpoint's own fp16 GEMM weights
@@ -261,24 +289,52 @@ class Model(TokenizerMixin):
                     if t.device != self.device or t.dtype != dt or not t.is_contiguous():
                         raise ValueError("raw16 tensors must be contiguous fp16 (w1, w2) / fp32 (g1, g2) on the "
                                          "model device")
-            arr = (_lib.CExact16Layer * self.cfg.n_layers)(
-                *[_lib.CExact16Layer(r.w1.data_ptr(), r.w2.data_ptr(), r.g1.data_ptr(), r.g2.data_ptr())
-                  for r in raw])
-            _lib.check(self._lib.tvr_model_set_exact16(self._h, arr), "tvr_model_set_exact16")
-            self._x16_c = arr
             ru = self.weights.raw16_unembed
             if ru is not None:
                 wu, gf = ru
                 if wu.device != self.device or wu.dtype != torch.float16 or not wu.is_contiguous() or \
                         gf.device != self.device or gf.dtype != torch.float32:
                     raise ValueError("raw16_unembed must be (fp16 [V, d], fp32 [d]) contiguous on the model device")
-                _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, wu.data_ptr(), gf.data_ptr()),
-                           "tvr_model_set_exact16_unembed")
+            arr = (_lib.CExact16Layer * self.cfg.n_layers)(
+                *[_lib.CExact16Layer(r.w1.data_ptr(), r.w2.data_ptr(), r.g1.data_ptr(), r.g2.data_ptr())
+                  for r in raw])
+        # the engine re-plans the x2f16 weight planes on a (de)tach: hipMalloc / the conversion kernels run on
+        # the current device, which must be the model's
+        with torch.cuda.device(self.device):
+            try:
+                if on:
+                    self._x16_c = arr  # the engine keeps the binding from here on, even if the re-plan fails
+                    _lib.check(self._lib.tvr_model_set_exact16(self._h, arr), "tvr_model_set_exact16")
+                    if ru is not None:
+                        _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, wu.data_ptr(), gf.data_ptr()),
+                                   "tvr_model_set_exact16_unembed")
+                else:
+                    _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, None, None),
+                               "tvr_model_set_exact16_unembed")
+                    _lib.check(self._lib.tvr_model_set_exact16(self._h, None), "tvr_model_set_exact16")
+                    self._x16_c = None
+            finally:
+                # the engine records the binding before it re-plans, and a failed re-plan (e.g. the planes do
+                # not fit) leaves it in the fp32 mode: mirror what the engine holds, error or not
+                self.exact16 = bool(on)
+                self.gemm = _lib.GEMM_NAMES.get(self._lib.tvr_model_get_gemm(self._h), self.gemm)
+
+    def _fall_back(self, what: str, err: Exception) -> bool:
+        """Move to the next GEMM path without the x2f16 range limit after a
+        failed range check: exact-fp16 → processed weights (x2f16, 3 products:
+        LayerNorm's output, bounded by sqrt(d_model), is the A operand again),
+        x2f16 → x3bf16 (no range limit).  False when there is none left."""
+        if self.gemm != "x2f16":
+            return False
+        if self.exact16:
+            self.set_exact16(False)  # the engine re-plans the x2f16 planes on the processed weights
+            path = "x2f16 (processed weights)"
         else:
-            _lib.check(self._lib.tvr_model_set_exact16_unembed(self._h, None, None), "tvr_model_set_exact16_unembed")
-            _lib.check(self._lib.tvr_model_set_exact16(self._h, None), "tvr_model_set_exact16")
-            self._x16_c = None
-        self.exact16 = bool(on)
+            self.set_gemm("x3bf16")
+            path = "x3bf16"
+        self.range_fallbacks.append((what, path))
+        warnings.warn(f"{what}: {err} -- retrying on {path}", RuntimeWarning, stacklevel=3)
+        return True
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -303,10 +303,12 @@ def process_to_engine(cfg: PythiaConfig, sd: HFStateDict, device=None,
     layers, raw = [], ([] if raw16 else None)
     for l in range(cfg.n_layers):
         p = f"gpt_neox.layers.{l}."
-        # the raw tensors are read before _process_layer pops them (free_source)
-        layers.append(_process_layer(cfg, lambda n, p=p: take(p + n) if not free_source or n not in _RAW_NAMES
-                                     else _take_keep(sd, p + n, dev, dtype), raw))
-        if free_source and raw is not None:
+        # with raw16 the raw tensors are read twice (the raw copy, then the processing): kept in sd until the
+        # layer is done, then popped (free_source)
+        keep = free_source and raw is not None
+        layers.append(_process_layer(cfg, lambda n, p=p: _take_keep(sd, p + n, dev, dtype)
+                                     if keep and n in _RAW_NAMES else take(p + n), raw))
+        if keep:
             for n in _RAW_NAMES:
                 sd.pop(p + n, None)
     wu_raw, gf = take("embed_out.weight"), take("gpt_neox.final_layer_norm.weight")

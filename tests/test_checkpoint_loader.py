@@ -106,6 +106,20 @@ def test_processing_of_loaded_checkpoint(tmp_path, tiny):
     assert W.process_to_engine(cfg, got, raw16=False).raw16 is None
 
 
+@pytest.mark.parametrize("raw16", [False, True])
+def test_free_source_empties_the_state_dict(tmp_path, tiny, raw16):
+    """free_source pops every tensor it processed, with or without the raw fp16 copies (the raw
+    GEMM weights were kept alive when raw16 was off), and the result equals processing a kept dict."""
+    cfg, sd = tiny
+    got = W.load_hf_safetensors(write_checkpoint(tmp_path, cfg, sd), cfg)
+    ref = W.process_to_engine(cfg, dict(got), raw16=raw16)
+    out = W.process_to_engine(cfg, got, free_source=True, raw16=raw16)
+    assert got == {}
+    for x, y in zip(out.tensors(), ref.tensors()):
+        assert torch.equal(x, y)
+    assert (out.raw16 is not None) == raw16
+
+
 @pytest.mark.gpu
 def test_model_from_checkpoint_matches_state_dict(tmp_path, tiny):
     cfg, sd = tiny
