@@ -91,6 +91,11 @@ KERNELS = {"f32": "gemm_f32_nt_kernel (v_mfma_f32_32x32x2_f32; all three fused e
            "x2f16": "gemm_pingpong_kernel<ACT_X2F16> (2-plane fp16 split activations written by their producers, "
                     "LDS-DMA staging with counted waits, 4 phases per k-tile, two wave groups one barrier apart, "
                     "3 products on v_mfma_f32_16x16x32_f16, fp32 accumulate; all three fused epilogues)",
+           "x2f16-exact16": "gemm_pingpong_kernel<ACT_X2F16, WX> (2-plane fp16 split activations written by their "
+                            "producers against ONE exact fp16 weight plane (the checkpoint's own), 2 products on "
+                            "v_mfma_f32_16x16x32_f16, fp32 accumulate; wide wave tile (4 x 2 waves of 64 x 128), "
+                            "LDS-DMA staging with counted waits, 2 phases per k-tile over 3 LDS buffers (4 when "
+                            "sliced), two wave groups one barrier apart; all three fused epilogues)",
            "bf16": "gemm_pingpong_kernel<ACT_BF16> (bf16 weights and activations, LDS-DMA staging with counted "
                    "waits, two wave groups one barrier apart, v_mfma_f32_16x16x32_bf16, fp32 accumulate; all "
                    "three fused epilogues)"}
@@ -827,7 +832,7 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": KERNELS[args.gemm],
+            "kernel": KERNELS["x2f16-exact16" if (args.gemm == "x2f16" and model.exact16) else args.gemm],
             "achieved": round(achieved, 2),
             "peak": round(peak, 1),
             "unit": "TFLOP/s",

@@ -1269,7 +1269,9 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
   const int tiles = (V + 255) / 256, chunk = final_chunk(m, fmt, out_logits);
   for (int s = 0; s < n; s += chunk) {
     const int cn = std::min(chunk, n - s);
-    const bool xu = fused && use_x16(m) && m->wux.h;  // the exact-fp16 unembed (statistics only)
+    // the exact-fp16 unembed: LNPre(x) o gamma_f against the raw W_U (the statistics are invariant to the
+    // per-row constant this leaves in the logits; the logits path removes it below)
+    const bool xu = use_x16(m) && m->wux.h;
     TVR_TRY(launch_lnpre(resid, d, d_rows + s, xf, d, cn, d, c.ln_eps, fmt, st, m, nullptr, nullptr, 0,
                          xu ? m->gf : nullptr));
     if (fused) {
@@ -1296,7 +1298,18 @@ int run_final(tvr_model* m, const float* resid, const int32_t* d_rows, const int
     e.bias = m->b_unembed;
     e.out0 = lg;
     e.ld0 = V;
-    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, fmt, m->wu, d, cn, V, d, e, st, m));
+    TVR_TRY(launch_gemm(EPI_BIAS, xf, d, fmt, xu ? m->wux : m->wu, d, cn, V, d, e, st, m));
+    if (xu) {
+      // TL's W_U' = center_unembed(fold_ln(W_U)): (LNPre(x) o gamma_f) W_U^T + b_U' differs from TL's logits by
+      // -LNPre(x) . (the vocab mean of the d-centred rows), one constant per row, and TL's logits have mean 0 over
+      // the vocabulary (W_U' and b_U' are centred over it): subtract each row's mean
+      const bool v4 = ((uintptr_t)lg & 15) == 0 && V % 4 == 0;
+      if (v4)
+        hipLaunchKernelGGL(center_rows_kernel<true>, dim3((cn + 3) / 4), dim3(256), 0, st, lg, lg, cn, V);
+      else
+        hipLaunchKernelGGL(center_rows_kernel<false>, dim3((cn + 3) / 4), dim3(256), 0, st, lg, lg, cn, V);
+      TVR_HIP(hipGetLastError());
+    }
     ProfSpan ps(m, st);
     hipLaunchKernelGGL(row_stats_kernel, dim3(cn), dim3(STATS_THREADS), 0, st, lg, V, V,
                        d_targets ? d_targets + s : nullptr, out_prob ? out_prob + s : nullptr,
@@ -1502,7 +1515,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   const size_t nu = (size_t)c.d_vocab * c.d_model;
   const int np = mode == TVR_GEMM_X3BF16 ? 3 : mode == TVR_GEMM_X2F16 ? 2 : 1;
   const size_t nqk = (size_t)2 * c.d_model * c.d_model;  // BF16: W1's Q / K rows as an fp16 plane
-  const size_t total = np * ((n1 + (mode == TVR_GEMM_X2F16 && m->x16 ? 0 : n2)) * L + nu) +
+  const size_t total = np * ((mode == TVR_GEMM_X2F16 && m->x16 ? 0 : n1 + n2) * L + nu) +
                        (mode == TVR_GEMM_BF16 ? nqk * L : 0);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
@@ -1511,17 +1524,16 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
                                    " bytes) do not fit");
   }
   // every GEMM weight matrix in order: w1[0], w2[0], ..., w1[L-1], w2[L-1], wu — in X2F16 with exact-fp16
-  // weights bound (tvr_model_set_exact16) without the w2 planes: the O + MLP-out GEMM reads the raw w2
-  // (12B: 19 GB not allocated); w1's planes stay (the linearised entry's G reads the processed rows)
-  const bool skip_w2 = mode == TVR_GEMM_X2F16 && m->x16;
+  // weights bound (tvr_model_set_exact16) without the w1 / w2 planes: every QKV + MLP-in, O + MLP-out and
+  // linearised-entry G GEMM reads the raw fp16 rows (2.8B: 5.9 + 4.2 GB, 12B: 26 + 19 GB not allocated)
+  const bool skip_x16 = mode == TVR_GEMM_X2F16 && m->x16;
   std::vector<MatW*> mats;
   std::vector<size_t> sizes;
-  for (int l = 0; l < L; ++l) {
-    mats.push_back(&m->w1[l]); sizes.push_back(n1);
-    if (!skip_w2) {
-      mats.push_back(&m->w2[l]);
-      sizes.push_back(n2);
-    }
+  for (int l = 0; l < L && !skip_x16; ++l) {
+    mats.push_back(&m->w1[l]);
+    sizes.push_back(n1);
+    mats.push_back(&m->w2[l]);
+    sizes.push_back(n2);
   }
   mats.push_back(&m->wu); sizes.push_back(nu);
   if (mode == TVR_GEMM_BF16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
@@ -2290,6 +2302,9 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
   const size_t o_raw = cv.take<float>(any_lin ? (size_t)Rc * c.d_mlp : 0);
   const size_t o_vact = cv.take<float>(any_lin ? (size_t)n_vectors * d : 0);  // vectors in the activation format
   const size_t o_g = cv.take<float>((size_t)lin_max_nv * m->D1);
+  // exact-fp16 weights: one layer's G rows (centred vectors x LN1 / LN2 gamma, activation format)
+  const bool lin_x16 = any_lin && use_x16(m);
+  const size_t o_vg = cv.take<float>(lin_x16 ? (size_t)2 * lin_max_nv * d : 0);
   TVR_TRY(ensure_workspace(m, cv.off, st));
   char* base = m->ws;
   UploadBatch ub;
@@ -2402,7 +2417,29 @@ int tvr_patch_sweep(tvr_model* m, tvr_trace* trace, const tvr_site* sites, int32
     eg.skinny = 1;
     int rc = TVR_OK;
     const int nqk = fmt == ACT_BF16 && !m->w1qk.empty() ? 2 * d : 0;  // bf16: Q / K columns on fp16 operands
-    if (nqk > 0) {
+    if (lin_x16) {
+      // G = v W1'^T on the raw fp16 W1 (one plane, 2 products): rows ((v - mean) o gamma1 | gamma2), lin_entry.hpp
+      uint16_t* vg1 = (uint16_t*)(base + o_vg);
+      uint16_t* vg2 = vg1 + (size_t)2 * lin_nv[l] * d;
+      hipLaunchKernelGGL(lin_gamma_rows_kernel, dim3((lin_nv[l] + 3) / 4), dim3(256), 0, st, vectors, d,
+                         (const int32_t*)(base + o_lin_vids) + lin_vid_off[l], m->g1[l], m->g2[l], vg1, vg2,
+                         lin_nv[l], m->range_flag);
+      rc = hipGetLastError() == hipSuccess ? TVR_OK : fail(TVR_ERR_HIP, "lin_gamma_rows_kernel launch");
+      GemmEpi ex = eg;
+      ex.a_rows = nullptr;  // the rows are the layer's vectors in order
+      const int q = 3 * d;  // first MLP-in column: it and the columns after it read the gamma2 rows
+      if (rc == TVR_OK && q % 256 == 0) {
+        ex.a2 = vg2;
+        ex.a2_col = q;
+        rc = launch_gemm(EPI_BIAS, vg1, d, fmt, m->w1x[l], d, lin_nv[l], D1, d, ex, st, m);
+      } else if (rc == TVR_OK) {  // two launches (d % 256 != 0: the tiny test model)
+        rc = launch_gemm(EPI_BIAS, vg1, d, fmt, m->w1x[l], d, lin_nv[l], q, d, ex, st, m);
+        GemmEpi e2 = ex;
+        e2.out0 = ex.out0 + q;
+        if (rc == TVR_OK)
+          rc = launch_gemm(EPI_BIAS, vg2, d, fmt, m->w1x[l].rows((size_t)q * d), d, lin_nv[l], D1 - q, d, e2, st, m);
+      }
+    } else if (nqk > 0) {
       rc = launch_gemm(EPI_BIAS, vact + d, d, ACT_F16, m->w1qk[l], d, lin_nv[l], nqk, d, eg, st, m);
       GemmEpi e2 = eg;
       e2.out0 = eg.out0 + nqk;

@@ -64,9 +64,10 @@ __global__ void embed_kernel(const int32_t* __restrict__ tokens,
 
 // dst[r] = src[r] - mean(src[r]) (one wave per row, d % 4 == 0): the exact-fp16 weight path's residual
 // stream carries one extra constant per row (engine.hip tvr_model, x16), which the TL residual lacks
-// V4: src and dst 16-B aligned, d % 4 == 0 (float4 accesses); else element-wise (a caller's offset view)
+// V4: src and dst 16-B aligned, d % 4 == 0 (float4 accesses); else element-wise (a caller's offset view).
+// src == dst allowed (each lane reads an element before it writes it, in both passes)
 template <bool V4>
-__global__ void center_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int rows, int d) {
+__global__ void center_rows_kernel(const float* src, float* dst, int rows, int d) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + wave;
   if (r >= rows) return;

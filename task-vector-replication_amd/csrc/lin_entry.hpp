@@ -257,4 +257,34 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
   }
 }
 
+
+// The rows of G on the exact-fp16 weights (tvr_model_set_exact16): the processed W1' = fold_ln(W1) has
+// W1'[n][k] = W1[n][k] gamma_k - m_n, so for ANY vector v
+//     v W1'^T = ((v - mean(v)) o gamma) W1^T
+// (sum_k (v_k - mean) gamma_k W1[n][k] = sum_k v_k gamma_k W1[n][k] - m_n sum_k v_k), with gamma1 for the
+// Q | K | V columns and gamma2 for the MLP-in ones: row r of out1 / out2 (x2f16 activation format, [rows][2][d]
+// halves) is vector vids[r] centred and scaled, for the one-plane GEMM against the raw W1.  One wave per row.
+__global__ void __launch_bounds__(256) lin_gamma_rows_kernel(const float* __restrict__ v, int d,
+                                                            const int32_t* __restrict__ vids,
+                                                            const float* __restrict__ g1, const float* __restrict__ g2,
+                                                            uint16_t* __restrict__ out1, uint16_t* __restrict__ out2,
+                                                            int rows, unsigned* flag) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + wave;
+  if (r >= rows) return;
+  const float* x = v + (size_t)vids[r] * d;
+  float s = 0.f;
+  for (int c = 4 * lane; c < d; c += 256) {
+    const f32x4 q = *(const f32x4*)(x + c);
+    s += (q[0] + q[1]) + (q[2] + q[3]);
+  }
+  const float mean = wave_sum(s) / (float)d;
+  for (int c = 4 * lane; c < d; c += 256) {
+    const f32x4 q = *(const f32x4*)(x + c) - mean;
+    const f32x4 a = *(const f32x4*)(g1 + c) * q, b = *(const f32x4*)(g2 + c) * q;
+    store_act4<ACT_X2F16>(out1 + (size_t)r * 2 * d + c, d, a[0], a[1], a[2], a[3], flag);
+    store_act4<ACT_X2F16>(out2 + (size_t)r * 2 * d + c, d, b[0], b[1], b[2], b[3], flag);
+  }
+}
+
 }  // namespace tvr

@@ -147,17 +147,17 @@ FV_LAYER, FV_HEADS = 10, 10  # C4: the function vector of the top-10 heads with 
 _C4 = {}
 
 
-def c4_reference():
+def c4_reference(fp16=False):
     """Pythia-6.9B (32 layers, std-0.05 weights) and the oracle's side of the
     C4 chain, computed once: extraction over 64 five-shot prompts, the CIE of
     12 prompts over layers 0..10, 16, 31, the top-10 FV heads of layers <= 10,
     the FV's top-5 accuracy on 50 zero-shot prompts."""
-    if _C4:
-        return _C4
+    if fp16 in _C4:
+        return _C4[fp16]
     name = "pythia-6.9b"
     cfg = tvr_amd.get_config(name)
     b = _Builder(cfg)
-    oracle = streamed_oracle(cfg)
+    oracle = streamed_oracle(cfg, fp16=fp16)
     H = cfg.n_heads
     task = tvr_amd.tasks.synthetic_task(50, cfg.d_vocab, seed=101)
     random.seed(5)
@@ -182,16 +182,16 @@ def c4_reference():
 
     def acc(tops):
         return sum(f in [dec(int(t)) for t in row] for f, row in zip(firsts, tops)) / len(zs)
-    _C4.update(cfg=cfg, name=name, oracle=oracle, ex=ex, mean_ref=mean_ref, mean32=mean32, prompts=prompts,
-               answers=answers, layers=layers, cie_ref=cie_ref, cmax=cie_ref.abs().max().item(),
-               set_ref=sorted(divmod(int(i), H) for i in top.indices[:FV_HEADS]),
-               gap=(top.values[FV_HEADS - 1] - top.values[FV_HEADS]).item(), contexts=contexts,
-               acc_ref=(acc(base_top[:, :5]), acc(oracle.added_topk(zs, FV_LAYER, fv_ref, 5))))
-    return _C4
+    _C4[fp16] = dict(cfg=cfg, name=name, oracle=oracle, ex=ex, mean_ref=mean_ref, mean32=mean32, prompts=prompts,
+                     answers=answers, layers=layers, cie_ref=cie_ref, cmax=cie_ref.abs().max().item(),
+                     set_ref=sorted(divmod(int(i), H) for i in top.indices[:FV_HEADS]),
+                     gap=(top.values[FV_HEADS - 1] - top.values[FV_HEADS]).item(), contexts=contexts,
+                     acc_ref=(acc(base_top[:, :5]), acc(oracle.added_topk(zs, FV_LAYER, fv_ref, 5))))
+    return _C4[fp16]
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("gemm", ["x2f16", "bf16"])
+@pytest.mark.parametrize("gemm", ["x2f16", "x2f16-fp16w", "bf16"])
 def test_c4_function_vector_pipeline(gemm, monkeypatch):
     """C4 at full depth.  x2f16 (fp32-accurate): the north star's fp32 bars —
     extraction 1e-4, CIE 1e-4 max|CIE| + 1e-7, the top-10 FV head set and the
@@ -202,10 +202,16 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
     oracle with the engine's operand roundings, measured on the same sites):
     the 10th and 11th oracle CIE values are ~1e-3 of max |CIE| apart, two
     orders of magnitude inside bf16's ~1e-1 CIE noise, so the top-10 set is a
-    fp32-accurate requirement (asserted on x2f16) and reported for bf16."""
-    r = c4_reference()
+    fp32-accurate requirement (asserted on x2f16) and reported for bf16.
+    ``x2f16-fp16w``: fp16-valued weights (the released checkpoints' dtype) —
+    the exact-fp16 GEMMs, incl. the linearised entry's G on the raw W1 — at the
+    x2f16 bars against the oracle on the same weights."""
+    fp16 = gemm.endswith("-fp16w")
+    gemm = gemm.replace("-fp16w", "")
+    r = c4_reference(fp16)
     cfg, H = r["cfg"], r["cfg"].n_heads
-    model = tvr_amd.Model.from_pretrained(r["name"], device="cuda", seed=0, std=STD, gemm=gemm)
+    model = tvr_amd.Model.from_pretrained(r["name"], device="cuda", seed=0, std=STD, gemm=gemm, fp16_weights=fp16)
+    assert model.exact16 == fp16
     try:
         ex, prompts, answers, layers, cmax = r["ex"], r["prompts"], r["answers"], r["layers"], r["cmax"]
         mean_eng = model.project_heads(E.sum_last_z(model, ex)) / len(ex)
@@ -221,7 +227,8 @@ def test_c4_function_vector_pipeline(gemm, monkeypatch):
         fv_eng = E.assemble_task_vector(mean_eng, cie_chain.to(mean_eng.device), FV_LAYER, FV_HEADS)
         acc_eng = tuple(E.check_accuracy_of_task_vector(fv_eng, FV_LAYER, r["contexts"], 5, model=model))
         overlap = len(set(set_eng) & set(r["set_ref"]))
-        print(f"C4 {gemm}: extraction max-abs rel {e_mean:.3e}; CIE max |CIE| {cmax:.3e}, |err| / max|CIE| at "
+        print(f"C4 {gemm}{' fp16 weights' if fp16 else ''}: extraction max-abs rel {e_mean:.3e}; CIE max |CIE| "
+              f"{cmax:.3e}, |err| / max|CIE| at "
               f"layers 0/16/31 {err[0].max() / cmax:.2e} / {err[16].max() / cmax:.2e} / {err[31].max() / cmax:.2e}, "
               f"all {err.max() / cmax:.2e}; top-{FV_HEADS} heads (layer <= {FV_LAYER}) oracle {r['set_ref']}, engine "
               f"{set_eng} ({overlap} shared; oracle 10th-11th gap {r['gap']:.2e}), chain {set_chain}; FV top-5 "
@@ -306,32 +313,38 @@ def oracle_layer_sweeps(oracle, b, seqs, contexts, answers, vector):
 
 
 @pytest.mark.timeout(900)
-def test_c2_layer_sweeps_full_depth_x2f16():
+@pytest.mark.parametrize("fp16", [False, True], ids=["processed", "fp16w"])
+def test_c2_layer_sweeps_full_depth_x2f16(fp16):
     """C2 (scratch2.py:114-127 accuracy and :135-150 Δprob sweeps, the repo's
     headline plots) on the whole 32-layer Pythia-2.8B with std-0.05 weights,
     52 zero-shot prompts x 32 layers, against the fp64 streamed oracle: the
     per-layer accuracy list identical, Δprob within 1e-4 of the largest |Δprob|
     + 1e-7 (the north star's fp32 bars).  The vector is the reference's
     layered_vectors[-1] (late binding, App. B1) of the oracle's own extraction
-    (scratch2.py:156-163: 2048 six-shot prompts there, 64 here)."""
+    (scratch2.py:156-163: 2048 six-shot prompts there, 64 here).  ``fp16w``:
+    fp16-valued weights, as the released checkpoints and the bench — the
+    exact-fp16 GEMMs (2 products) and the exact-fp16 fused-statistics unembed,
+    the path the bench's C2 number runs."""
     name = "pythia-2.8b"
     cfg = tvr_amd.get_config(name)
     b = _Builder(cfg)
-    oracle = streamed_oracle(cfg)
+    oracle = streamed_oracle(cfg, fp16=fp16)
     random.seed(3)
     ex = tvr_amd.prompts.sample_icl_prompts(b, list(tvr_amd.tasks.letter_to_caps), ARROW, ",", 64, 6)
     layered = E.gather_head_activations_to_layers(oracle.mean_activation(ex)).float()  # [L, d] fp32
     vec = layered[-1].double()
     contexts, seqs, answers = c2_contexts(oracle, b, cfg, vec)
     acc_ref, dp_ref, margin = oracle_layer_sweeps(oracle, b, seqs, contexts, answers, vec)
-    model = tvr_amd.Model.from_pretrained(name, device="cuda", seed=0, std=STD, gemm="x2f16")
+    model = tvr_amd.Model.from_pretrained(name, device="cuda", seed=0, std=STD, gemm="x2f16", fp16_weights=fp16)
+    assert model.exact16 == fp16
     try:
         acc = E.apply_layered_vectors_to_zero_shot(layered.cuda(), contexts, ARROW, model=model)
         dp = E.apply_layered_vectors_to_zero_shot_by_probability(layered.cuda(), contexts, ARROW, model=model)
         dp = dp.cpu().double()
         dmax = dp_ref.abs().max().item()
         err = (dp - dp_ref).abs().max().item()
-        print(f"C2 {name} x2f16, 32 layers: accuracy engine {acc}\n  oracle {acc_ref}\n  Δprob max |ref| {dmax:.3e}, "
+        print(f"C2 {name} x2f16{' fp16 weights' if fp16 else ''}, 32 layers: accuracy engine {acc}\n  oracle {acc_ref}\n"
+              f"  Δprob max |ref| {dmax:.3e}, "
               f"|err| {err:.2e} = {err / dmax:.2e} of max; smallest oracle top-1 margin {margin:.2e}")
         informative = [a for a in acc_ref if 0 < a < 1]
         assert len(informative) >= 4 and dmax > 1e-3, (acc_ref, dmax)

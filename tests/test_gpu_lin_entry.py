@@ -158,17 +158,23 @@ def test_lin_entry_equals_full_entry_gemm(deep, gemm, monkeypatch):
 #   regression in code both entry paths share shows against the oracle, not
 #   only against the other path; and the paths within 5e-2 of p_max of each
 #   other (each rounds its own way).
-WIDE = [("pythia-2.8b", "x2f16", 4), ("pythia-12b", "x2f16", 10), ("pythia-6.9b", "bf16", 5)]
+# (fp16w: fp16-valued weights — the exact-fp16 GEMMs, the linearised entry's G = v W1'^T as ((v - mean) o gamma)
+# W1^T on the raw rows, lin_entry.hpp lin_gamma_rows_kernel)
+WIDE = [("pythia-2.8b", "x2f16", 4), ("pythia-12b", "x2f16", 10), ("pythia-6.9b", "bf16", 5),
+        ("pythia-2.8b", "x2f16-fp16w", 4), ("pythia-12b", "x2f16-fp16w", 10)]
 
 
 @pytest.mark.slow
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name,gemm,kshot", WIDE, ids=[f"{n}-{g}" for n, g, _ in WIDE])
 def test_lin_entry_at_headline_widths(name, gemm, kshot, monkeypatch):
+    fp16 = gemm.endswith("-fp16w")
+    gemm = gemm.replace("-fp16w", "")
     cfg = tvr_amd.get_config(name).with_(n_layers=3)
-    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1, fp16=fp16)
     tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
     model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok, gemm=gemm)
+    assert model.exact16 == fp16
     prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 2, kshot, seed=1234)
     clean = model.forward_clean(prompts, topk=1)
     answers = [[int(t)] for t in clean["topk"][:, 0].tolist()]  # p ~ 1e-9 for random pairs: use the argmax
@@ -223,17 +229,23 @@ def test_lin_entry_at_headline_widths(name, gemm, kshot, monkeypatch):
 
 @pytest.mark.slow
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name,gemm,kshot", [("pythia-2.8b", "x2f16", 4), ("pythia-6.9b", "bf16", 5)],
-                         ids=["pythia-2.8b-x2f16", "pythia-6.9b-bf16"])
+@pytest.mark.parametrize("name,gemm,kshot", [("pythia-2.8b", "x2f16", 4), ("pythia-6.9b", "bf16", 5),
+                                             ("pythia-2.8b", "x2f16-fp16w", 4)],
+                         ids=["pythia-2.8b-x2f16", "pythia-6.9b-bf16", "pythia-2.8b-x2f16-fp16w"])
 def test_lin_entry_head_shard_at_headline_widths(name, gemm, kshot, monkeypatch):
     """One rank's share of an 8-way head split (heads h = 0 mod 8): 4 distinct
     vectors per entry layer, so the linearised entry's G = v W1^T runs on
     gemm_skinny_kernel (<= 16 rows) at the real K / N (2560 / 17920, 4096 /
-    28672), against the full entry GEMM at the bars of the test above."""
+    28672), against the full entry GEMM at the bars of the test above.  fp16w:
+    the one-plane G on the raw W1 with NON-centred vectors (the random means
+    below: the centring in lin_gamma_rows_kernel is what makes it exact)."""
+    fp16 = gemm.endswith("-fp16w")
+    gemm = gemm.replace("-fp16w", "")
     cfg = tvr_amd.get_config(name).with_(n_layers=3)
-    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1)
+    sd = tvr_amd.weights.synth_hf_state_dict(cfg, seed=0, std=0.1, fp16=fp16)
     tok = tvr_amd.tokenizer.SyntheticTokenizer(cfg.d_vocab)
     model = tvr_amd.Model.from_hf_state_dict(cfg, sd, device="cuda", tokenizer=tok, gemm=gemm)
+    assert model.exact16 == fp16
     prompts, _ = tvr_amd.prompts.synthetic_cie_prompts(model, 2, kshot, seed=1234)
     answers = [int(t) for t in model.forward_clean(prompts, topk=1)["topk"][:, 0].tolist()]
     pmax = model.forward_clean(prompts, targets=answers)["prob"].max().item()
