@@ -143,6 +143,9 @@ def parse():
                     help="N=1: the other BASELINE.json configs timed after the headline, reported under 'configs' "
                          "(C2 = the Pythia-2.8B layer sweeps on the headline model, C4 = the Pythia-6.9B bf16 "
                          "function-vector suite per task, C5 = the Pythia-12B 36x40 10-shot CIE sweep); '' skips them")
+    ap.add_argument("--c5-layers", dest="c5_layers", type=int, default=0,
+                    help="rehearsals only: C5 on the first N of Pythia-12B's 36 layers (two 12B replicas on one GPU); "
+                         "the workload string says so, and 0 (default) is the BASELINE config")
     ap.add_argument("--launch-check", dest="launch_check", action="store_true",
                     help="only the rank launch, rendezvous and max-over-ranks timing (no GPU work; CPU test)")
     return ap.parse_args()
@@ -333,7 +336,7 @@ def config_c2(model, mean, peak, reps=3):
     return out
 
 
-def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
+def config_c5(args, dev, peak, world=1, rank=0, emulate=0, return_cie=False):
     """C5: Pythia-12B, the full 36 x 40 CIE sweep of 12
     shuffled 10-shot prompts (T = 33): 17,280 patched prompts per step.  At
     N > 1 the SAME sweep is split across the ranks as the headline's C3 is
@@ -341,12 +344,18 @@ def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
     all-reduce of the [L, H] sums; strong scaling, max-over-ranks time);
     ``emulate`` times rank 0's share of that split on one GPU.  Seeded
     synthetic weights and means; one warmup step, ``steps`` timed.  F_alg per
-    SURVEY §8d."""
+    SURVEY §8d.  ``args.c5_layers`` > 0 (rehearsals): the first that many
+    layers only.  ``return_cie``: the step's all-reduced [L, H] CIE sums too
+    (tests/test_gpu_distributed.py compares the sharded sweep with one process)."""
     import tvr_amd
     from tvr_amd.distributed import balanced_site_shard
     from tvr_amd.experiments import causal_indirect_effect_sums
     t0 = time.time()
-    model = tvr_amd.Model.from_pretrained("pythia-12b", device=dev, seed=0, gemm=args.gemm,
+    cfg12 = tvr_amd.get_config("pythia-12b")
+    layers = getattr(args, "c5_layers", 0)
+    if layers:
+        cfg12 = cfg12.with_(n_layers=layers)
+    model = tvr_amd.Model.from_pretrained("pythia-12b", cfg=cfg12, device=dev, seed=0, gemm=args.gemm,
                                           fp16_weights=args.weights == "fp16")
     cfg = model.cfg
     x16 = bool(model.exact16)
@@ -362,7 +371,7 @@ def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
         if world > 1:
             dist.all_reduce(cie)
         return cie
-    step()
+    cie = step()
     steps = max(1, min(args.steps, 2))
     if world > 1:
         dist.barrier()
@@ -380,12 +389,13 @@ def config_c5(args, dev, peak, world=1, rank=0, emulate=0):
     peak_all = peak * (1 if emulate else world)
     del model
     torch.cuda.empty_cache()
-    return {"workload": c5_workload(world, emulate, len(sites) if sites else 0),
+    extra = {"cie": cie.cpu()} if return_cie else {}
+    return {"workload": c5_workload(world, emulate, len(sites) if sites else 0, L),
             "n_gpus": world, "scaling": "strong", "rank_elapsed_s": [round(x, 4) for x in rt] if rt else None,
             "units_per_step": units, "steps": steps, "ms_per_step": round(sec * 1e3, 1),
             "value": round(rate, 2), "unit": "patched prompts/s", "gflop_per_site": round(f_alg / 1e9, 2),
             "site_tflops": round(rate * f_alg / 1e12, 2), "site_frac": round(rate * f_alg / 1e12 / peak_all, 4),
-            "exact16_gemms": x16, "model_build_s": round(build_s, 1)}
+            "exact16_gemms": x16, "model_build_s": round(build_s, 1), **extra}
 
 
 def rank_times(el, dev):
@@ -406,12 +416,13 @@ def c4_workload(world: int) -> str:
     return base
 
 
-def c5_workload(world: int, emulate: int = 0, n_sites_rank: int = 0) -> str:
-    base = "pythia-12b CIE sweep 36x40 sites, 12 prompts/step, 10-shot, T=33"
+def c5_workload(world: int, emulate: int = 0, n_sites_rank: int = 0, layers: int = 36) -> str:
+    cut = "" if layers == 36 else f" (REHEARSAL: the first {layers} of 36 layers)"
+    base = f"pythia-12b CIE sweep {layers}x40 sites, 12 prompts/step, 10-shot, T=33{cut}"
     if emulate:
         return (f"pythia-12b CIE sweep, rank 0's share of a {emulate}-GPU split (sites in balanced layer-pair blocks "
-                f"per rank: {n_sites_rank} of 1440 sites), 12 prompts/step, 10-shot, T=33 (planning emulation on "
-                "one GPU)")
+                f"per rank: {n_sites_rank} of {layers * 40} sites), 12 prompts/step, 10-shot, T=33{cut} (planning "
+                "emulation on one GPU)")
     if world > 1:
         base += ", sites in balanced layer-pair blocks per rank"
     return base

@@ -1515,8 +1515,14 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
   const size_t nu = (size_t)c.d_vocab * c.d_model;
   const int np = mode == TVR_GEMM_X3BF16 ? 3 : mode == TVR_GEMM_X2F16 ? 2 : 1;
   const size_t nqk = (size_t)2 * c.d_model * c.d_model;  // BF16: W1's Q / K rows as an fp16 plane
+  // diagnostic knobs, read per call, for the bf16 bars' negative controls (tests/test_gpu_full_depth.py
+  // test_bf16_bars_reject_a_wrong_bf16_path) — never set in production: TVR_DEBUG_BF16_QK=0 drops the fp16
+  // Q / K operands (the Q / K columns run on bf16 like the rest), TVR_DEBUG_BF16_TRUNC=1 builds the bf16
+  // weight planes by truncation instead of round-to-nearest-even
+  const bool bf16_qk16 = env_int("TVR_DEBUG_BF16_QK", 1) != 0;
+  const bool bf16_trunc = env_int("TVR_DEBUG_BF16_TRUNC", 0) != 0;
   const size_t total = np * ((mode == TVR_GEMM_X2F16 && m->x16 ? 0 : n1 + n2) * L + nu) +
-                       (mode == TVR_GEMM_BF16 ? nqk * L : 0);
+                       (mode == TVR_GEMM_BF16 && bf16_qk16 ? nqk * L : 0);
   if (hipMalloc(&m->planes, total * sizeof(uint16_t)) != hipSuccess) {
     m->planes = nullptr;
     (void)hipGetLastError();
@@ -1536,7 +1542,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
     sizes.push_back(n2);
   }
   mats.push_back(&m->wu); sizes.push_back(nu);
-  if (mode == TVR_GEMM_BF16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
+  if (mode == TVR_GEMM_BF16 && bf16_qk16) {  // the fp16 Q / K planes: one scale per layer from max |W_QK|
     for (int l = 0; l < L; ++l) {
       mats.push_back(nullptr);
       sizes.push_back(nqk);
@@ -1600,7 +1606,7 @@ int tvr_model_set_gemm(tvr_model* m, int32_t mode, void* stream) {
       hipLaunchKernelGGL(split_planes_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
       w = MatW{w.f, p, nullptr, n, 1.0f};
     } else if (mode == TVR_GEMM_BF16) {
-      hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n);
+      hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, st, w.f, p, n, (int)bf16_trunc);
       w = MatW{w.f, nullptr, p, n, 1.0f};
     } else {
       hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, st, w.f, scale[i], p, n);
@@ -2604,7 +2610,7 @@ int tvr_weight_planes(int32_t fmt, const float* w, float scale, uint16_t* out, s
   if (fmt == TVR_GEMM_X2F16)
     hipLaunchKernelGGL(split_planes_f16_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, scale, out, n);
   else
-    hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, out, n);
+    hipLaunchKernelGGL(bf16_plane_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, w, out, n, 0);
   TVR_HIP(hipGetLastError());
   return TVR_OK;
 }

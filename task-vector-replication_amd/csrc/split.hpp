@@ -191,9 +191,10 @@ __global__ void act_rows_bf16_f16_kernel(const float* __restrict__ a, int lda, u
 }
 
 // W [n] fp32 -> one bf16 plane (TVR_GEMM_BF16 weights, load time)
-__global__ void bf16_plane_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, size_t n) {
+// (trunc: round toward zero — a diagnostic, the negative control of the bf16 parity bars)
+__global__ void bf16_plane_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, size_t n, int trunc) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    out[i] = bf16_bits(w[i]);
+    out[i] = trunc ? (uint16_t)(__float_as_uint(w[i]) >> 16) : bf16_bits(w[i]);
 }
 
 // W [n] fp32 -> one fp16 plane of scale * W (scale a power of two putting

@@ -8,10 +8,17 @@ single-process engine results:
 * mean_activation_sharded (contiguous prompt split, all-reduce) == sum_last_z / n, projected
 * the layer sweeps and the FV layer sweep with (prompt, layer) sites
   round-robin + all_gather                                      == the unsharded sweeps
+* bench.py's C5 leg (Pythia-12B shape, 10-shot, depth cut to 6 of 36 layers so
+  two replicas share one GPU): the 2-rank balanced site split (one whole layer
+  pair per rank + the third pair split by head, one all-reduce) == the same
+  sweep in one process.
+
+Rendezvous through a file in pytest's tmp dir (no probed port that another
+process could take between the probe and the bind).
 """
 import os
 import random
-import socket
+import types
 
 import pytest
 import torch
@@ -20,12 +27,6 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 WORLD = 2
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _setup():
@@ -62,32 +63,41 @@ def _run(sharded: bool):
             "fv": E.check_accuracy_of_added_task_vector_by_layer(fv, task, 5, model)}
 
 
-def _worker(rank, port, q):
+def _worker(rank, init, job, q):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=WORLD)
     try:
-        q.put((rank, _run(True)))
+        q.put((rank, job(rank)))
     except Exception as e:  # surface the failure in the parent instead of hanging it
         q.put((rank, repr(e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_entry_points_on_the_engine():
+def _ranks(tmp_path, job, timeout=180):
+    """job(rank) on WORLD spawned gloo ranks (file rendezvous); their results by rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    init = f"file://{tmp_path / 'rendezvous'}"
+    procs = [ctx.Process(target=_worker, args=(r, init, job, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     try:
-        results = dict(q.get(timeout=180) for _ in range(WORLD))
+        return dict(q.get(timeout=timeout) for _ in range(WORLD))
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+
+
+def _sharded(rank):
+    return _run(True)
+
+
+def test_sharded_entry_points_on_the_engine(tmp_path):
+    results = _ranks(tmp_path, _sharded)
     for r in range(WORLD):
         assert isinstance(results[r], dict), results[r]
     ref = _run(False)
@@ -99,3 +109,35 @@ def test_sharded_entry_points_on_the_engine():
         assert got["acc"] == ref["acc"]
         assert torch.allclose(got["dprob"], ref["dprob"], rtol=0, atol=1e-6)
         assert got["fv"] == ref["fv"]
+
+
+C5_ARGS = types.SimpleNamespace(gemm="x2f16", weights="fp16", prompts=4, steps=1, c5_layers=6)
+
+
+def _c5_rank(rank):
+    import bench
+    res = bench.config_c5(C5_ARGS, "cuda:0", 1.0, world=WORLD, rank=rank, return_cie=True)
+    return {k: res[k] for k in ("cie", "workload", "units_per_step", "rank_elapsed_s")}
+
+
+@pytest.mark.timeout(600)
+def test_c5_leg_two_ranks_equals_one_process(tmp_path):
+    """bench.config_c5 at world 2 (the sharded C5 leg had never completed): Pythia-12B's
+    width / 40 heads / 10-shot T = 33 prompts, 6 layers, fp16-valued weights (exact-fp16 GEMMs, sliced
+    accumulation, linearised entry).  balanced_site_shard gives each rank one whole layer pair and half the
+    heads of the third; one all-reduce; the result must equal the single-process sweep's CIE sums."""
+    import bench
+    results = _ranks(tmp_path, _c5_rank, timeout=540)
+    for r in range(WORLD):
+        assert isinstance(results[r], dict), results[r]
+    ref = bench.config_c5(C5_ARGS, "cuda:0", 1.0, world=1, return_cie=True)
+    cie1 = ref["cie"].double()
+    big = cie1.abs().max().item()
+    assert big > 0 and (cie1 != 0).double().mean().item() > 0.9
+    for r in range(WORLD):
+        got = results[r]
+        assert "REHEARSAL" in got["workload"] and got["units_per_step"] == 4 * 6 * 40
+        assert len(got["rank_elapsed_s"]) == WORLD
+        err = (got["cie"].double() - cie1).abs().max().item()
+        print(f"C5 rehearsal rank {r}: |sharded - one process| {err:.2e} of max |CIE sum| {big:.3e}")
+        assert err <= 1e-5 * big + 1e-9, (r, err, big)

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
       if (path == "bf16" || path == "bf16pp") {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
         hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, dim3(8192), dim3(256), 0, 0, A, s.K, A2, s.M, s.K,
                            (unsigned*)nullptr);  // [M][2][K] halves, plane 0 = bf16(A)
-        hipLaunchKernelGGL(bf16_plane_kernel, dim3(8192), dim3(256), 0, 0, W, W2, (size_t)s.N * s.K);
+        hipLaunchKernelGGL(bf16_plane_kernel, dim3(8192), dim3(256), 0, 0, W, W2, (size_t)s.N * s.K, 0);
       }
       GemmEpi e{}; e.out0 = C; e.ld0 = s.N;
       int grid = 0;
