@@ -109,6 +109,10 @@ def parse():
     ap.add_argument("--model", default="pythia-2.8b")
     ap.add_argument("--prompts", type=int, default=12, help="CIE prompts per GPU per step")
     ap.add_argument("--kshot", type=int, default=4)
+    ap.add_argument("--c4-prompts", dest="c4_prompts", action="store_true",
+                    help="profiling: the headline sweep on C4's shuffled string prompts (a synthetic 50-pair task, "
+                         "--kshot demos, tokenised: T=23 at 5-shot) instead of the single-token ones, so a rocprofv3 "
+                         "pass of it is C4's CIE sweep at C4's own prompt length (tools/prof_cmd.sh)")
     ap.add_argument("--extract", type=int, default=2048,
                     help="prompts of the mean extraction (a1, C2's N = 2048, 6-shot, T = 28) that supplies the CIE "
                          "means; timed separately (extraction prompts/s, capture kernel GB/s); 0 = seeded random "
@@ -730,8 +734,16 @@ def main():
     if emulate and shard == "prompts":
         raise SystemExit("--emulate-world times a strong split: --shard sites or heads")
     everything = [(l, h) for l in range(cfg.n_layers) for h in range(cfg.n_heads)]
+    if args.c4_prompts:  # C4's CIE prompts (config_c4): shuffled string prompts of a synthetic task, tokenised
+        import random
+        random.seed(1)
+        task = tvr_amd.tasks.synthetic_task(50, cfg.d_vocab, seed=101)
+        sp, sa = tvr_amd.experiments.generate_shuffled_prompts(task, model, args.prompts, args.kshot,
+                                                               tvr_amd.tasks.ARROW)
+        c4_prompts = [model.to_tokens(p)[0].tolist() for p in sp], [a[0] for a in sa]
     if shard in ("sites", "heads"):  # C3: the same prompts everywhere, this rank's share of the sites
-        prompts, answers = tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234)
+        prompts, answers = (c4_prompts if args.c4_prompts else
+                            tvr_amd.prompts.synthetic_cie_prompts(model, args.prompts, args.kshot, seed=1234))
         n_split = emulate or world
         sites = (balanced_site_shard(cfg.n_layers, cfg.n_heads, rank, n_split) if shard == "sites" else
                  [(l, h) for l in range(cfg.n_layers) for h in strided_shard(cfg.n_heads, rank, n_split)])
@@ -831,7 +843,7 @@ def main():
         "dtype": DTYPE_X16 if (args.gemm == "x2f16" and model.exact16) else DTYPES[args.gemm],
         "data": f"synthetic (seeded {args.model}-shaped weights, "
                 f"{'fp16-valued as the released checkpoints' if args.weights == 'fp16' else 'fp32-valued'}; "
-                f"seeded single-token shuffled-label prompts)",
+                f"{'C4 shuffled string prompts of a synthetic task' if args.c4_prompts else 'seeded single-token shuffled-label prompts'})",
         "config": {
             "workload": workload,
             "sites_per_step": units_total,
