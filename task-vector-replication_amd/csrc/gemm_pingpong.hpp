@@ -126,6 +126,13 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_WX_WIDE
 #define TVR_PP_WX_WIDE 2
 #endif
+// bf16 / fp16 operands (one plane each, BK 64): 1 the wide four-phase tile (pp_tile_wt: reads per phase 8 / 8
+// / 4 / 4 fragments against pp_tile's 12 / 4 / 8 / 0), 0 (default) pp_tile.  The wide form holds 8 weight
+// column tiles x 2 k-groups (+32 VGPRs: 256 with 11 spilled) and measured slower on the probe's shapes, qkv / o
+// 1,193 / 1,250 vs 1,258 / 1,351 TF (profiles/r06/bf16_wide_probe_r06g.txt), so pp_tile stays
+#ifndef TVR_PP_BF16_WIDE
+#define TVR_PP_BF16_WIDE 0
+#endif
 // One-plane weights, unsliced: 1 the two-phase, three-buffer K loop (pp_tile P2), 0 the four-phase one
 #ifndef TVR_PP_WX_2PHASE
 #define TVR_PP_WX_2PHASE 0
@@ -796,20 +803,32 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 #ifndef TVR_WT_SGB
 #define TVR_WT_SGB 1
 #endif
-template <int EPI, bool VEC, int VAR, bool SL, bool TWO = false>
+template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool TWO = false>
 __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int lda, size_t aps,
                                            const uint16_t* __restrict__ W, int ldw, float acc_scale, int M, int N,
                                            const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part,
                                            int has_part, unsigned long long st0, unsigned long long sr0) {
-  using F = PlanarFmt<ACT_X2F16>;
+  // FMT: ACT_X2F16 with one exact weight plane (two activation planes, BK 32), or one bf16 / fp16 plane of each
+  // operand (BK 64: the fragments' second index is the k-group instead of the plane); both 2 A fragments per
+  // 16-row tile per k-tile, the weight 1 (x2f16) or 2 (bf16 / fp16) per 16-column tile
+  using F = PlanarFmt<FMT>;
   using frag = typename F::frag;
-  constexpr int BK = F::BK;            // 32 halves: 64 B per plane row
-  constexpr int CPR = BK / 8;          // 4 chunks of 16 B per row
-  constexpr int RPP = 64 / CPR;        // 16 rows per 1 KB piece
-  constexpr int PPP = 128 / RPP;       // 8 pieces per plane per region
+  constexpr int NPL = F::NPL;          // activation planes (2 x2f16, 1 bf16 / fp16)
+  constexpr int BK = F::BK;            // halves per plane row per k-tile: 128 B of K in both forms
+  constexpr int KG = BK / 32;          // k-groups (fragments along K) per k-tile
+  constexpr int CPR = BK / 8;          // 16-B chunks per plane row
+  constexpr int RPP = 64 / CPR;        // rows per 1 KB piece
+  constexpr int PPP = 128 / RPP;       // pieces per plane per region
+  constexpr int WP = PPP / 8;          // weight pieces per wave per region (1 x2f16, 2 bf16)
   constexpr int PL = 256 * BK;         // halves per plane per buffer
-  constexpr int BUF = 3 * PL;          // A hi / lo planes + one weight plane
+  constexpr int BUF = (NPL + 1) * PL;  // activation planes + one weight plane
   constexpr int NBUF = TWO ? 3 : 2;    // TWO: the two-phase loop's three buffers (below)
+  static_assert(!TWO || FMT == ACT_X2F16, "three 64 KB bf16 buffers do not fit the LDS");
+  static_assert(NPL * KG == 2, "two A fragments per 16-row tile per k-tile");
+  static_assert(!SL || FMT == ACT_X2F16, "the sliced accumulation is an x2f16 form");
+  // vmcnt of every phase: the pieces issued after the awaited region (two activation regions of 2 pieces and
+  // two weight regions of WP per k-tile; four phases: 4 + 2 WP, the prologue's first wait 4 + 3 WP)
+  constexpr int VM = 4 + 2 * WP, VM0 = 4 + 3 * WP;
   constexpr int DUMMY = NBUF * BUF;
   constexpr int LDS_HALVES = (NBUF * BUF + 512) > PP_EPI_LDS ? (NBUF * BUF + 512) : PP_EPI_LDS;
   static_assert(LDS_HALVES * 2 <= 160 * 1024, "LDS budget");
@@ -829,7 +848,7 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
   for (int R = 0; R < 4; ++R) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int pi = R >= 2 ? wave_s : 2 * wave_s + s;
+      const int pi = R >= 2 ? WP * wave_s + (WP > 1 ? s : 0) : 2 * wave_s + s;
       const int plane = pi / PPP, x0 = (pi % PPP) * RPP;  // region row of the piece's first row
       const int trow0 = R < 2 ? ((x0 >> 5) << 6) + (x0 & 31) + 32 * R : ((x0 >> 6) << 7) + (x0 & 63) + 64 * (R - 2);
       const int row = trow0 + lane / CPR;
@@ -840,7 +859,7 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
         dst[R][s] = plane * PL + trow0 * BK;
       } else {
         src[R][s] = W + (size_t)min(n0 + row, N - 1) * ldw + chunk * 8;
-        dst[R][s] = 2 * PL + trow0 * BK;
+        dst[R][s] = NPL * PL + trow0 * BK;
       }
     }
   }
@@ -849,25 +868,30 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
     const int koff = live ? (kbeg + kt) * BK : 0;
     const int boff = (TWO ? kt % 3 : kt & 1) * BUF;
 #pragma unroll
-    for (int s = 0; s < (R >= 2 ? 1 : 2); ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
+    for (int s = 0; s < (R >= 2 ? WP : 2); ++s) glds16(src[R][s] + koff, lds + (live ? boff + dst[R][s] : DUMMY));
   };
 
-  // fragment offsets: plane f of the wave's first row tile / the weight plane at its first column tile
-  int aoff[2];
+  // fragment offsets: fragment f (x2f16: plane f; bf16: k-group f) of the wave's first row tile, k-group g of
+  // the weight plane at its first column tile
+  int aoff[2], woff[KG];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    const int ra = wr * 64 + (lane & 15), c = lane >> 4;
-    aoff[f] = f * PL + ra * BK + ((c ^ planar_g<CPR>(ra)) << 3);
+    const int p = NPL == 2 ? f : 0, g = NPL == 2 ? 0 : f;
+    const int ra = wr * 64 + (lane & 15), c = 4 * g + (lane >> 4);
+    aoff[f] = p * PL + ra * BK + ((c ^ planar_g<CPR>(ra)) << 3);
   }
-  const int rb = wc * 128 + (lane & 15);
-  const int woff = 2 * PL + rb * BK + (((lane >> 4) ^ planar_g<CPR>(rb)) << 3);
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const int rb = wc * 128 + (lane & 15), c = 4 * g + (lane >> 4);
+    woff[g] = NPL * PL + rb * BK + ((c ^ planar_g<CPR>(rb)) << 3);
+  }
 
   f32x4 acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
-  frag fa[4][2], fw[8];
+  frag fa[4][2], fw[8][KG];
 
   // live 16-row slices of the wave's 64 rows (rows past M are copies of row M - 1): the PART loop skips the
   // padding slices' fragment reads and MFMAs (staging and barriers stay)
@@ -882,7 +906,9 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
   auto read_w = [&](const uint16_t* base, int j0, auto part) {
     if (decltype(part)::value && vi == 0) return;
 #pragma unroll
-    for (int j = j0; j < j0 + 4; ++j) fw[j] = *(const frag*)(base + woff + j * 16 * BK);
+    for (int j = j0; j < j0 + 4; ++j)
+#pragma unroll
+      for (int g = 0; g < KG; ++g) fw[j][g] = *(const frag*)(base + woff[g] + j * 16 * BK);
   };
   [[maybe_unused]] f32x4 tc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   // one phase's cluster: row tiles i0, i0 + 1 x column tiles j0 .. j0 + NJ - 1 (4, or 8 in the two-phase
@@ -901,7 +927,7 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int jj = u & 1, pz = u >> 1;  // MFMA u: product pz (0: a1 w0, 1: a0 w0) of tile (i, j + jj)
-          s[q & 1][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j + jj], fa[i][pz == 0 ? 1 : 0],
+          s[q & 1][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j + jj][0], fa[i][pz == 0 ? 1 : 0],
                                                                  pz == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : s[q & 1][jj],
                                                                  0, 0, 0);
           if (TVR_WT_SGB) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -923,12 +949,18 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
         if (decltype(part)::value && i >= vi) continue;
         f32x4 c = acc[i][j];
         if constexpr (SL) {
-          f32x4 s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][0], s, 0, 0, 0);
+          f32x4 s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], s, 0, 0, 0);
           c = slice_add(c, s);
+        } else if constexpr (FMT == ACT_X2F16) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+        } else if constexpr (FMT == ACT_F16) {  // k-group 0, then 1 (pp_tile's order)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][KG - 1], fa[i][1], c, 0, 0, 0);
         } else {
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][0], fa[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][KG - 1], fa[i][1], c, 0, 0, 0);
         }
         acc[i][j] = c;
       }
@@ -964,7 +996,7 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
     stage(0, 1);
     stage(2, 1);
     stage(3, 1);
-    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM0) : "memory");
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -1008,22 +1040,22 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
       const uint16_t* cur = lds + (kt & 1) * BUF;
       // q1: rows 0-31 x cols 0-63
       read_w(cur, 0, part);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // W_hi(kt) (q4 of kt-2), read in q2
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");  // W_hi(kt) (q4 of kt-2), read in q2
       stage(1, kt + 1);
       TVR_PP_CLUSTER(cluster(0, 0, part, 3, 2));  // (ci, cj): the previous phase's carried pair (q4: tiles (3, 2..3))
       // q2: rows 0-31 x cols 64-127
       read_w(cur, 4, part);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_hi(kt) (q1 of kt-1), read in q3
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");  // A_hi(kt) (q1 of kt-1), read in q3
       stage(0, kt + 2);
       TVR_PP_CLUSTER(cluster(0, 4, part, 1, 2));
       // q3: rows 32-63 x cols 64-127
       read_a(cur, 2, part);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1) (q2 of kt-1), read in q4
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");  // A_lo(kt+1) (q2 of kt-1), read in q4
       stage(2, kt + 2);
       TVR_PP_CLUSTER(cluster(2, 4, part, 1, 6));
       // q4: rows 32-63 x cols 0-63; reads the next k-tile's A_lo (its cluster needs nothing read here)
       read_a(lds + ((kt + 1) & 1) * BUF, 0, part);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // W_lo(kt+1) (q3 of kt-1), read in q1
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");  // W_lo(kt+1) (q3 of kt-1), read in q1
       stage(3, kt + 2);
       TVR_PP_CLUSTER(cluster(2, 0, part, 3, 6));
     }
@@ -1050,9 +1082,9 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
       pe.out0 = part;
       pe.ld0 = 256;
       pe.out_rows = nullptr;
-      pp_epilogue_lds<EPI, ACT_X2F16, VAR == 8, 4, 8>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+      pp_epilogue_lds<EPI, FMT, VAR == 8, 4, 8>(pe, acc, L, 0, 0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
     } else {
-      pp_epilogue_lds<EPI, ACT_X2F16, VAR == 8, 4, 8>(ep, acc, L, m0, n0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
+      pp_epilogue_lds<EPI, FMT, VAR == 8, 4, 8>(ep, acc, L, m0, n0, M - m0, N - n0, wr, wc, lane, t, acc_scale);
     }
     if ((VAR == 6 || VAR == 8) && ep.stamps && t == 0) {
       unsigned long long* o = ep.stamps + 4 * blockIdx.x;
@@ -1076,9 +1108,9 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
       GemmEpi pe = ep;
       pe.out0 = part;
       pe.ld0 = 256;
-      gemm_epilogue16t<EPI, ACT_X2F16, VEC, 4, 8>(pe, acc, M - m0, N - n0, wr * 64, wc * 128, lane);
+      gemm_epilogue16t<EPI, FMT, VEC, 4, 8>(pe, acc, M - m0, N - n0, wr * 64, wc * 128, lane);
     } else {
-      gemm_epilogue16t<EPI, ACT_X2F16, VEC, 4, 8>(ep, acc, M, N, m0 + wr * 64, n0 + wc * 128, lane);
+      gemm_epilogue16t<EPI, FMT, VEC, 4, 8>(ep, acc, M, N, m0 + wr * 64, n0 + wc * 128, lane);
     }
     if (ep.stamps && t == 0) {
       ep.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - st0;
@@ -1095,15 +1127,18 @@ __device__ __forceinline__ void pp_tile_any(const uint16_t* __restrict__ A, int 
                                             int M, int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk,
                                             float* part, int has_part, unsigned long long st0,
                                             unsigned long long sr0) {
-  constexpr bool wide = WX && FMT == ACT_X2F16 &&
-                        (VAR == 16 || VAR == 20 || (VAR != 17 && TVR_PP_WX_WIDE && (VAR == 0 || VAR == 6 || VAR == 8)));
+  // bf16 / fp16 (one plane each): the wide four-phase tile when TVR_PP_BF16_WIDE (VAR 16 / 17 force it / pp_tile)
+  constexpr bool wide = (WX && FMT == ACT_X2F16 &&
+                         (VAR == 16 || VAR == 20 || (VAR != 17 && TVR_PP_WX_WIDE && (VAR == 0 || VAR == 6 || VAR == 8)))) ||
+                        ((FMT == ACT_BF16 || FMT == ACT_F16) &&
+                         (VAR == 16 || (VAR != 17 && TVR_PP_BF16_WIDE && (VAR == 0 || VAR == 6 || VAR == 8))));
   // (the sliced form stays on four phases: the two-phase cluster keeps all 8 weight fragments live through
   // both clusters, 16 VGPRs more than the 252 the sliced four-phase form holds — it spilled 38)
-  constexpr bool two = VAR == 20 || (VAR != 16 && TVR_PP_WX_WIDE == 2 && !SL);
+  constexpr bool two = FMT == ACT_X2F16 && (VAR == 20 || (VAR != 16 && TVR_PP_WX_WIDE == 2 && !SL));
   constexpr int V = (VAR == 16 || VAR == 17 || VAR == 20) ? 0 : VAR;
   if constexpr (wide)
-    pp_tile_wt<EPI, VEC, V, SL, two>(A, lda, aps, W, ldw, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part, st0,
-                                     sr0);
+    pp_tile_wt<EPI, FMT, VEC, V, SL, two>(A, lda, aps, W, ldw, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part,
+                                          st0, sr0);
   else
     pp_tile<EPI, FMT, VEC, V, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part,
                                       st0, sr0);

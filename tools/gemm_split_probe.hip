@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (const auto& path : paths) {
-      if (path == "bf16" || path == "bf16pp") {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
+      if (path == "bf16" || path.rfind("bf16pp", 0) == 0) {  // one bf16 plane of A and of W (after every x2 path: they share A2 / W2)
         hipLaunchKernelGGL(act_rows_kernel<ACT_BF16>, dim3(8192), dim3(256), 0, 0, A, s.K, A2, s.M, s.K,
                            (unsigned*)nullptr);  // [M][2][K] halves, plane 0 = bf16(A)
         hipLaunchKernelGGL(bf16_plane_kernel, dim3(8192), dim3(256), 0, 0, W, W2, (size_t)s.N * s.K, 0);
@@ -227,9 +227,12 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 6>), dim3(grid), dim3(PP_THREADS), 0, 0,
                                A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
           }
-        } else if (path == "bf16pp") {
+        } else if (path == "bf16pp" || path == "bf16ppw" || path == "bf16ppn") {  // default / wide (VAR 16) / pp_tile (17)
           grid = gemm_pingpong_grid(s.M, s.N);
-          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16>), dim3(grid), dim3(PP_THREADS), 0, 0,
+          auto kb = path == "bf16ppw"   ? gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 16>
+                    : path == "bf16ppn" ? gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 17>
+                                        : gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 0>;
+          hipLaunchKernelGGL(kb, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
         } else if (path == "x2ps") {  // the 128x128 / 4-wave tile at the same shape (2 blocks per CU)
           grid = gemm_planar_grid<PlanarSmall>(s.M, s.N);
