@@ -17,8 +17,10 @@ from tvr_amd import experiments as E  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--weights", default="fp16", choices=["fp16", "fp32"],
+                help="fp16-valued weights (the bench's default: exact-fp16 GEMMs) or fp32-valued")
 a = ap.parse_args()
-model = tvr_amd.Model.from_pretrained("pythia-2.8b", device="cuda")
+model = tvr_amd.Model.from_pretrained("pythia-2.8b", device="cuda", fp16_weights=a.weights == "fp16")
 task, arrow = tvr_amd.tasks.letter_to_caps, tvr_amd.tasks.ARROW
 random.seed(0)
 mean = E.generate_mean_activation(task, arrow, model=model, num_contexts=64, len_contexts=6)
