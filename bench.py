@@ -806,7 +806,7 @@ def main():
     T = len(prompts[0])
     workload, scaling = describe_workload(args.model, cfg.n_layers, cfg.n_heads, args.prompts, args.kshot, T, world,
                                           shard, emulate, len(sites))
-    if model.exact16:  # another kernel instruction mix: counters of the 3-product runs do not apply
+    if model.exact16 and args.gemm == "x2f16":  # another kernel instruction mix: 3-product counters do not apply
         workload += ", fp16-valued weights (exact-fp16 GEMMs, 2 products)"
     pmc, traffic_src = pmc_summary(args.gemm, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -890,8 +890,8 @@ def main():
     }
     out["config"]["gemm"] = args.gemm
     out["config"]["weights"] = args.weights
-    out["config"]["exact16_gemms"] = bool(model.exact16)
-    if world == 1 and model.exact16 and not emulate and args.processed_leg:
+    out["config"]["exact16_gemms"] = bool(model.exact16 and args.gemm == "x2f16")  # (bf16 mode leaves them unused)
+    if world == 1 and model.exact16 and args.gemm == "x2f16" and not emulate and args.processed_leg:
         # the same sweep on the TL-processed weights (3 products: the path of fp32-valued checkpoints)
         model.set_exact16(False)
         npw = max(1, min(args.steps, 2))
