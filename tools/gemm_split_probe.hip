@@ -212,6 +212,23 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 8>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "x2pp6wx" || path == "x2pp6gwx") {  // anatomy of the one-plane (wide) kernel
+          grid = gemm_pingpong_grid(s.M, s.N);
+          GemmEpi eg = ee;
+          if (path == "x2pp6gwx") {
+            eg.n_split = (s.N * 3 / 7) & ~255;
+            eg.out1h = (uint16_t*)(C) + eg.n_split;
+            eg.ld1h = 2 * s.N;
+            eg.ps1h = s.N;
+            eg.range_flag = flag;
+            hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_SPLIT_GELU_ACT, ACT_X2F16, true, 6, false, false, true>),
+                               dim3(grid), dim3(PP_THREADS), 0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K,
+                               (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
+          } else {
+            hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 6, false, false, true>), dim3(grid),
+                               dim3(PP_THREADS), 0, 0, A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K,
+                               acc_scale, s.M, s.N, s.K, eg);
+          }
         } else if (path == "x2pp6" || path == "x2pp6g") {  // per-block anatomy (prologue / loop / epilogue)
           grid = gemm_pingpong_grid(s.M, s.N);
           GemmEpi eg = ee;
@@ -248,7 +265,8 @@ int main(int argc, char** argv) {
                              A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
         }
       };
-      if (path == "x2pp6" || path == "x2pp6g" || path == "x2pp8") {  // block anatomy: medians over blocks (cycles)
+      if (path == "x2pp6" || path == "x2pp6g" || path == "x2pp8" || path == "x2pp6wx" || path == "x2pp6gwx") {
+        // block anatomy: medians over blocks (cycles)
         for (int i = 0; i < 5; ++i) run(false);
         run(true);
         hipDeviceSynchronize();
