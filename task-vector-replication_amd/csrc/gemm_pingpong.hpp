@@ -799,7 +799,12 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 // after its last read, issued 6 phases before its first read and retired one phase before it by
 // vmcnt(6) (the pieces issued since: 1 + 2 + 2 + 1 in every phase), as pp_tile's rules.  Per output
 // element the MFMA sequence is pp_tile's (a1 w0, then a0 w0, k-slice by k-slice; sliced: the slice's sum
-// added once): bit-identical results.  A/B: TVR_PP_WX_WIDE=0, or VAR 16 / 17 (probe).
+// added once): bit-identical results.  A/B: TVR_PP_WX_WIDE=0, or VAR 16 / 17 (probe).  TWO (unsliced x2f16):
+// two phases of 32 MFMAs over three LDS buffers (the loop below).  FMT bf16 / fp16 (TVR_PP_BF16_WIDE, off):
+// the same schedule with one plane per operand at BK 64 (2 weight pieces per wave per region, vmcnt(8)).
+// Per-block anatomy (probe, VAR 6; profiles/r06/wide_tile_anatomy_r06l.jsonl): 2,143-2,365 cycles per
+// k-tile against 2,048 of MFMA issue, a QKV + MLP-in tile 2.6 % prologue / 84 % loop / 13.4 % epilogue.
+// TVR_WT_SGB=0 drops the sliced form's sched_group_barriers (A/B of the placement)
 #ifndef TVR_WT_SGB
 #define TVR_WT_SGB 1
 #endif
