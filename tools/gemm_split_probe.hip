@@ -212,6 +212,11 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 8>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
+        } else if (path == "bf16pp6") {  // anatomy of the bf16 kernel (pp_tile; one plane each, BK 64)
+          grid = gemm_pingpong_grid(s.M, s.N);
+          GemmEpi eg = ee;
+          hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 6>), dim3(grid), dim3(PP_THREADS), 0, 0,
+                             A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, eg);
         } else if (path == "x2pp6wx" || path == "x2pp6gwx") {  // anatomy of the one-plane (wide) kernel
           grid = gemm_pingpong_grid(s.M, s.N);
           GemmEpi eg = ee;
@@ -265,7 +270,8 @@ int main(int argc, char** argv) {
                              A, s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, flag, s.M, s.N, s.K, ee);
         }
       };
-      if (path == "x2pp6" || path == "x2pp6g" || path == "x2pp8" || path == "x2pp6wx" || path == "x2pp6gwx") {
+      if (path == "x2pp6" || path == "x2pp6g" || path == "x2pp8" || path == "x2pp6wx" || path == "x2pp6gwx" ||
+          path == "bf16pp6") {
         // block anatomy: medians over blocks (cycles)
         for (int i = 0; i < 5; ++i) run(false);
         run(true);
@@ -281,7 +287,8 @@ int main(int argc, char** argv) {
         std::sort(pro.begin(), pro.end()); std::sort(loop.begin(), loop.end()); std::sort(epi.begin(), epi.end());
         printf("{\"shape\": \"%s\", \"path\": \"%s\", \"prologue_cyc\": %.0f, \"loop_cyc\": %.0f, "
                "\"loop_cyc_per_ktile\": %.1f, \"epilogue_cyc\": %.0f, \"epilogue_p90\": %.0f}\n", s.name, path.c_str(),
-               pro[pro.size() / 2], loop[loop.size() / 2], loop[loop.size() / 2] / (s.K / 32), epi[epi.size() / 2],
+               pro[pro.size() / 2], loop[loop.size() / 2], loop[loop.size() / 2] / (s.K / (path == "bf16pp6" ? 64 : 32)),
+               epi[epi.size() / 2],
                epi[epi.size() * 9 / 10]);
         fflush(stdout);
         continue;
