@@ -137,6 +137,12 @@ constexpr int PP_SLICE_MIN_K = TVR_PP_SLICE_MIN_K;
 #ifndef TVR_PP_WX_2PHASE
 #define TVR_PP_WX_2PHASE 0
 #endif
+// pp_tile, two-plane operands (bf16 / fp16, unsliced x2f16): 1 read the NEXT k-tile's first two A row tiles
+// in q4 (into 4 extra fragments, +16 VGPRs), so the read segments are 8 / 4 / 8 / 4 fragments instead of
+// 12 / 4 / 8 / 0 (A_lo(t+1) is then retired in q3: one more counted wait); 0 the plain order.  VAR 21 flips it
+#ifndef TVR_PP_PF
+#define TVR_PP_PF 1
+#endif
 // (The add as four v_add_f32 in inline asm, to keep the SLP vectorizer from packing it into v_pk_add_f32,
 // read the MFMA results without the MFMA -> VALU wait states the compiler inserts for its own code: every
 // x2f16 result came out wrong on the GPU.  Plain C++: the compiler packs and places the waits.)
@@ -336,7 +342,7 @@ struct PpLds {
 // tile (acc * acc_scale, no bias) goes to part as a dense 256 x 256 tile
 // (split-K / stream-K), else the launch's fused epilogue.  (A separate int
 // flag: testing the pointer itself made hipcc spill 26-66 VGPRs.)
-template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX = false>
+template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX = false, bool PFOK = true>
 __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda, size_t aps,
                                         const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale, int M,
                                         int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk, float* part, int has_part,
@@ -434,6 +440,8 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
   frag fa[4][2], fwl[2][2], fwh[2][2];
+  constexpr bool PF = PFOK && ((TVR_PP_PF != 0) != (VAR == 21)) && !P2 && !WX && !(FMT == ACT_X2F16 && SL);
+  [[maybe_unused]] frag fx[2][2];  // PF: row tiles 0-1 of A_lo, read one phase early
 
   // 16-row slices of this wave's 128 rows that hold real rows (A rows past M
   // are staged as copies of row M - 1).  A wave with fewer than 8 runs the
@@ -442,12 +450,19 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
   // the last m-block of every launch, and most blocks of the small-M layer
   // sweeps (C2: M = 156 + 52 l rows in 256-row tiles).
   const int vi = __builtin_amdgcn_readfirstlane(min(8, max(0, (M - m0 - wr * 128 + 15) >> 4)));  // wave-uniform
-  auto read_a = [&](const uint16_t* base, int i0, auto part) {
+  auto read_a = [&](const uint16_t* base, int i0, auto part, int ifirst = 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (!decltype(part)::value || i0 + i < vi)
+      if (i >= ifirst && (!decltype(part)::value || i0 + i < vi))
 #pragma unroll
         for (int f = 0; f < 2; ++f) fa[i][f] = *(const frag*)(base + aoff[f] + (i0 + i) * 16 * BK);
+  };
+  auto read_fx = [&](const uint16_t* base, auto part) {  // PF: A row tiles 0-1 into fx
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (!decltype(part)::value || i < vi)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) fx[i][f] = *(const frag*)(base + aoff[f] + i * 16 * BK);
   };
   auto read_w = [&](const uint16_t* base, int j0, frag (&fw)[2][2], auto part) {
     if (decltype(part)::value && vi == 0) return;
@@ -560,22 +575,24 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       for (int j = 0; j < 2; ++j) {
         if (decltype(part)::value && i0 + i >= vi) continue;
         f32x4 c = acc[i0 + i][j0 + j];
+        const bool x = PF && i0 == 0 && i < 2;  // PF: row tiles 0-1 live in fx
+        const frag a0 = x ? fx[i & 1][0] : fa[i][0], a1 = x ? fx[i & 1][1] : fa[i][1];
         if constexpr (FMT == ACT_X2F16 && SL) {  // the slice's sum first, then one add (see above)
-          f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          if constexpr (!WX) t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], t, 0, 0, 0);
+          f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], a1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          if constexpr (!WX) t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], a0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], a0, t, 0, 0, 0);
           c = slice_add(c, t);
         } else if constexpr (FMT == ACT_X2F16) {  // small terms first; the big a0*w0 last
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], a1, c, 0, 0, 0);
           if constexpr (VAR != 15 && !WX)  // (VAR 15, probe timing: the product dropped on full staging)
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], a0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], a0, c, 0, 0, 0);
         } else if constexpr (FMT == ACT_F16) {
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], a0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][1], a1, c, 0, 0, 0);
         } else {
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][0], fa[i][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][1], fa[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][0], a0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j][1], a1, c, 0, 0, 0);
         }
         acc[i0 + i][j0 + j] = c;
       }
@@ -637,6 +654,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PF) read_fx(lds, std::integral_constant<bool, false>{});  // A_lo(0) rows 0-1 (retired above)
   if (wr == 1 && VAR != 3) {  // the group offset: waves 4-7 run one barrier behind
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -673,7 +691,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
     for (int kt = 0; kt < nk; ++kt) {
       const uint16_t* cur = lds + (kt & 1) * BUF;
       // q1: Q(A_lo, W_lo)
-      read_a(cur, 0, part);
+      read_a(cur, 0, part, PF ? 2 : 0);
       read_w(cur, 0, fwl, part);
       if constexpr (XS) {
         asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // W_hi(kt) (q1 of kt-1), read in q2
@@ -703,6 +721,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       TVR_PP_CLUSTER(mfma_quadrant(0, 2, fwh, part, 3, 0));
       // q3: Q(A_hi, W_hi)
       read_a(cur, 4, part);
+      if constexpr (PF) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1) (q3 of kt-1), read in q4
       stage(XS ? 2 : 0, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 2, fwh, part, 3, 2));
       // q4: Q(A_hi, W_lo)
@@ -713,6 +732,7 @@ __device__ __forceinline__ void pp_tile(const uint16_t* __restrict__ A, int lda,
       } else {
         if (VAR != 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A_lo(kt+1), W_lo(kt+1) (q3 / q4 of kt-1), read in q1
       }
+      if constexpr (PF) read_fx(lds + ((kt + 1) & 1) * BUF, part);  // A_lo(kt+1) rows 0-1, retired in q3
       stage(XS ? 0 : 2, kt + 2);
       TVR_PP_CLUSTER(mfma_quadrant(4, 0, fwl, part, 7, 2));
     }
@@ -1126,7 +1146,7 @@ __device__ __forceinline__ void pp_tile_wt(const uint16_t* __restrict__ A, int l
 
 // One tile of a launch: the wide-tile form for one-plane weights (TVR_PP_WX_WIDE 1: four phases, 2: two;
 // VAR 16 / 20 force the four / two-phase wide tile, 17 pp_tile), else pp_tile
-template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX>
+template <int EPI, int FMT, bool VEC, int VAR, bool SL, bool WX, bool SKM>
 __device__ __forceinline__ void pp_tile_any(const uint16_t* __restrict__ A, int lda, size_t aps,
                                             const uint16_t* __restrict__ W, int ldw, size_t wps, float acc_scale,
                                             int M, int N, const GemmEpi& ep, int m0, int n0, int kbeg, int nk,
@@ -1145,8 +1165,10 @@ __device__ __forceinline__ void pp_tile_any(const uint16_t* __restrict__ A, int 
     pp_tile_wt<EPI, FMT, VEC, V, SL, two>(A, lda, aps, W, ldw, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part,
                                           st0, sr0);
   else
-    pp_tile<EPI, FMT, VEC, V, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk, part, has_part,
-                                      st0, sr0);
+    // (the q4 prefetch, TVR_PP_PF, not in the stream-K form or the statistics epilogue: their extra VGPRs
+    // there spilled 4 / 8)
+    pp_tile<EPI, FMT, VEC, V, SL, WX, !SKM && EPI != EPI_STATS>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0,
+                                                                kbeg, nk, part, has_part, st0, sr0);
 }
 
 // K must be a multiple of BK (host-checked); any M, N.
@@ -1195,7 +1217,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
       const int nk = (int)min((long long)(nk_all - kbeg), it1 - it);
       int m0, n0;
       pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
-      pp_tile_any<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+      pp_tile_any<EPI, FMT, VEC, VAR, SL, WX, SKM>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                   ep.out0 + ((size_t)2 * g + seg) * PP_TILE_ELEMS, 1, st0, sr0);
       it += nk;
     };
@@ -1211,7 +1233,7 @@ gemm_pingpong_kernel(const uint16_t* __restrict__ A, int lda, size_t aps, const 
     pp_tile_coords(ep.tile_base + lt, nbm, nbn, m0, n0, gm);
     const int kbeg = (int)((long long)split * nk_all / S);
     const int nk = (int)((long long)(split + 1) * nk_all / S) - kbeg;  // this block's k-tiles
-    pp_tile_any<EPI, FMT, VEC, VAR, SL, WX>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
+    pp_tile_any<EPI, FMT, VEC, VAR, SL, WX, SKM>(A, lda, aps, W, ldw, wps, acc_scale, M, N, ep, m0, n0, kbeg, nk,
                                 ep.out0 + ((size_t)split * count + lt) * PP_TILE_ELEMS, S > 1, st0, sr0);
   }
 }

@@ -149,9 +149,10 @@ int main(int argc, char** argv) {
           grid = gemm_pingpong_grid(s.M, s.N);
           hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16>), dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, ee);
-        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12" || path == "x2pp13" || path == "x2pp15") {  // diagnostic variants
+        } else if (path == "x2pp1" || path == "x2pp2" || path == "x2pp3" || path == "x2pp4" || path == "x2pp12" || path == "x2pp13" || path == "x2pp15" || path == "x2pp21") {  // diagnostic variants (21: TVR_PP_PF flipped)
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kp = path == "x2pp1" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 1>
+                    : path == "x2pp21" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 21>
                     : path == "x2pp2" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 2>
                     : path == "x2pp4" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 4>
                     : path == "x2pp12" ? gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 12>
@@ -249,10 +250,12 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((gemm_pingpong_kernel<EPI_BIAS, ACT_X2F16, true, 6>), dim3(grid), dim3(PP_THREADS), 0, 0,
                                A2, s.K, (size_t)s.M * s.K, W2, s.K, (size_t)s.N * s.K, acc_scale, s.M, s.N, s.K, eg);
           }
-        } else if (path == "bf16pp" || path == "bf16ppw" || path == "bf16ppn") {  // default / wide (VAR 16) / pp_tile (17)
+        } else if (path == "bf16pp" || path == "bf16ppw" || path == "bf16ppn" || path == "bf16ppf") {
+          // default / wide (VAR 16) / pp_tile (17) / pp_tile with the q4 prefetch flipped (21, TVR_PP_PF)
           grid = gemm_pingpong_grid(s.M, s.N);
           auto kb = path == "bf16ppw"   ? gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 16>
                     : path == "bf16ppn" ? gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 17>
+                    : path == "bf16ppf" ? gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 21>
                                         : gemm_pingpong_kernel<EPI_BIAS, ACT_BF16, true, 0>;
           hipLaunchKernelGGL(kb, dim3(grid), dim3(PP_THREADS), 0, 0,
                              A2, 2 * s.K, (size_t)s.K, W2, s.K, (size_t)s.N * s.K, 1.0f, s.M, s.N, s.K, ee);
