@@ -946,15 +946,27 @@ int launch_lnpre(const float* x, int ldx, const int32_t* idx, void* y, int ldy, 
     return fail(TVR_ERR_INTERNAL, "lnpre: the gamma-scaled rows are an x2f16 model path");
   const int rows_per_block = 4;
   const dim3 grid((rows + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
-  if (fmt == ACT_X2F16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_X2F16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows, g1, g2, y2, m ? m->range_flag : nullptr);
-  else if (fmt == ACT_BF16)
-    hipLaunchKernelGGL(lnpre_kernel<ACT_BF16>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows, nullptr, nullptr, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL(lnpre_kernel<ACT_F32>, grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy,
-                       copy_rows, nullptr, nullptr, nullptr, nullptr);
+  // the row in registers: 10 float4 per lane up to d = 2560, 20 up to 5120 (d % 256 == 0), else three passes
+  const int nv = d % 256 != 0 ? 0 : d <= 2560 ? 10 : d <= 5120 ? 20 : 0;
+#define TVR_LNPRE(F, NV, ...) \
+  hipLaunchKernelGGL((lnpre_kernel<F, NV>), grid, block, 0, st, x, ldx, idx, y, ldy, rows, d, eps, stats, copy, copy_rows, __VA_ARGS__)
+#define TVR_LNPRE_NV(F, ...)                 \
+  if (nv == 10) {                            \
+    TVR_LNPRE(F, 10, __VA_ARGS__);           \
+  } else if (nv == 20) {                     \
+    TVR_LNPRE(F, 20, __VA_ARGS__);           \
+  } else {                                   \
+    TVR_LNPRE(F, 0, __VA_ARGS__);            \
+  }
+  if (fmt == ACT_X2F16) {
+    TVR_LNPRE_NV(ACT_X2F16, g1, g2, y2, m ? m->range_flag : nullptr);
+  } else if (fmt == ACT_BF16) {
+    TVR_LNPRE_NV(ACT_BF16, nullptr, nullptr, nullptr, nullptr);
+  } else {
+    TVR_LNPRE_NV(ACT_F32, nullptr, nullptr, nullptr, nullptr);
+  }
+#undef TVR_LNPRE_NV
+#undef TVR_LNPRE
   TVR_HIP(hipGetLastError());
   // fp32 rows in, rows out in the activation format (x2f16 / fp32 4 B; bf16 2 + the fp16 plane 2 B per element;
   // the gamma-scaled pair two x2f16 rows)

@@ -151,47 +151,103 @@ constexpr int PP_EPI_LDS = 128 * PP_EPI_LDR * 2;  // halves
 
 // EPI_STATS: the rows of one LDS half (acc * acc_scale, row stride
 // PP_EPI_LDR) reduced to the per-tile statistics of GemmEpi::stats instead of
-// being stored.  Wave w takes rows w, w + 8, ...; lane l holds columns
-// 4l .. 4l+3 of the tile (+ bias b4), so every reduction is one butterfly over
-// the wave: the max, sum(exp(x - max)), and stats_k rounds of (value desc,
-// column asc) argmax with the winner removed from its lane.  The tile's
-// columns are [col0, col0 + Nlim), Nlim % 4 == 0 (host-checked).
+// being stored: per row the max, sum(exp(x - max)) and stats_k rounds of (value
+// desc, column asc) argmax.  Four threads per row (512 threads, 128 rows): the
+// quad's thread q scans columns 16 i + 4 q (i = 0 .. 15, + bias) in ascending
+// order from LDS, and the quad combines with two DPP steps — one pass for the
+// max, one for the exp sum and the first argmax, one more per further round,
+// whose candidates are the columns ordered after the previous winner.  (Round
+// 5's form, one wave per row with a 64-lane shuffle butterfly per statistic and
+// round, spent most of the epilogue in dependent ds_bpermute chains: 32 rows
+// per wave, 12 + 12 K shuffles each.)  The tile's columns are [col0, col0 +
+// min(Nlim, 256)), Nlim % 4 == 0 (host-checked).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_QUAD_X1 = 0xB1, DPP_QUAD_X2 = 0x4E;  // quad_perm [1,0,3,2], [2,3,0,1]
+__device__ __forceinline__ void quad_argmax(float& bv, int& bi) {
+  argmax_merge(bv, bi, dpp_f<DPP_QUAD_X1>(bv), dpp_i<DPP_QUAD_X1>(bi));
+  argmax_merge(bv, bi, dpp_f<DPP_QUAD_X2>(bv), dpp_i<DPP_QUAD_X2>(bi));
+}
 __device__ __forceinline__ void pp_stats_rows(const GemmEpi& ep, const float* L, int grow0, int col0, int rows,
-                                              int Nlim, f32x4 b4, int t) {
-  const int wave = t >> 6, lane = t & 63, c4 = 4 * lane;
-  const bool live = c4 < Nlim;
+                                              int Nlim, int t, float acc_scale) {
+  const int r = t >> 2, q = t & 3;
+  if (r >= rows) return;  // quad-uniform
+  Nlim = min(Nlim, 256);  // (N - col0: the tile's own columns)
   const int K = ep.stats_k, rec = 2 + 2 * K, tile = col0 >> 8;
-  for (int r = wave; r < rows; r += PP_THREADS / 64) {
-    f32x4 v = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    if (live) v = *(const f32x4*)(L + r * PP_EPI_LDR + c4) + b4;
-    const int m = grow0 + r;
-    const float mx = wave_max(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-    float se = 0.f;
-    if (live) se = (expf(v[0] - mx) + expf(v[1] - mx)) + (expf(v[2] - mx) + expf(v[3] - mx));
-    se = wave_sum(se);
-    float* o = ep.stats + ((size_t)m * ep.stats_tiles + tile) * rec;
-    if (ep.targets && ep.tlogit && live) {
-      const int q = ep.targets[m] - col0 - c4;
-      if (q >= 0 && q < 4) ep.tlogit[m] = q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
-    }
-    unsigned taken = live ? 0u : 0xFu;
-    for (int j = 0; j < K; ++j) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
+  const float* Lr = L + r * PP_EPI_LDR;
+  const float* bias = ep.bias ? ep.bias + col0 : nullptr;
+  // the accumulators are stored unscaled (scaling all 128 of a wave's in registers before the first half's
+  // reduction spilled 28-41 VGPRs): acc * acc_scale, then + bias, each rounded as the other epilogues do
+  auto elem = [&](float a, float b) { return __fadd_rn(__fmul_rn(a, acc_scale), b); };
+  auto chunk = [&](int i) {  // columns 16 i + 4 q .. + 3 (+ bias)
+    const int c = 16 * i + 4 * q;
+    const f32x4 a = *(const f32x4*)(Lr + c);
+    const f32x4 b = bias ? *(const f32x4*)(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    return f32x4{elem(a[0], b[0]), elem(a[1], b[1]), elem(a[2], b[2]), elem(a[3], b[3])};
+  };
+  const int nc = (Nlim - 4 * q + 15) >> 4;  // this thread's live chunks
+  float mx = -INFINITY;
+#pragma unroll 2
+  for (int i = 0; i < nc; ++i) {
+    const f32x4 v = chunk(i);
+    mx = fmaxf(mx, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+  }
+  mx = fmaxf(mx, dpp_f<DPP_QUAD_X1>(mx));
+  mx = fmaxf(mx, dpp_f<DPP_QUAD_X2>(mx));
+  float se = 0.f, bv = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll 2
+  for (int i = 0; i < nc; ++i) {
+    const f32x4 v = chunk(i);
+    se += (expf(v[0] - mx) + expf(v[1] - mx)) + (expf(v[2] - mx) + expf(v[3] - mx));
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (!((taken >> q) & 1u)) argmax_merge(bv, bi, v[q], col0 + c4 + q);
-      wave_argmax(bv, bi);
-      const int own = bi - col0 - c4;
-      if (own >= 0 && own < 4) taken |= 1u << own;
-      if (lane == 0) {
-        o[2 + j] = bv;
-        o[2 + K + j] = __int_as_float(bi);
+    for (int e = 0; e < 4; ++e)
+      if (v[e] > bv) {  // ascending columns: the first of equal values stays
+        bv = v[e];
+        bi = col0 + 16 * i + 4 * q + e;
+      }
+  }
+  se += dpp_f<DPP_QUAD_X1>(se);  // (a + b) == (b + a): every lane of the quad holds the same sum
+  se += dpp_f<DPP_QUAD_X2>(se);
+  const int m = grow0 + r;
+  float* o = ep.stats + ((size_t)m * ep.stats_tiles + tile) * rec;
+  if (q == 0) {
+    o[0] = mx;
+    o[1] = se;
+    if (ep.targets && ep.tlogit) {
+      const int tc = ep.targets[m] - col0;
+      if (tc >= 0 && tc < Nlim) ep.tlogit[m] = elem(Lr[tc], bias ? bias[tc] : 0.f);
+    }
+  }
+  for (int j = 0; j < K; ++j) {
+    if (j > 0) {  // the best column after the previous winner (pv, pi) in (value desc, column asc) order
+      const float pv = bv;
+      const int pi = bi;
+      bv = -INFINITY;
+      bi = 0x7fffffff;
+#pragma unroll 2
+  for (int i = 0; i < nc; ++i) {
+        const f32x4 v = chunk(i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = col0 + 16 * i + 4 * q + e;
+          if ((v[e] < pv || (v[e] == pv && c > pi)) && v[e] > bv) {
+            bv = v[e];
+            bi = c;
+          }
+        }
       }
     }
-    if (lane == 0) {
-      o[0] = mx;
-      o[1] = se;
+    quad_argmax(bv, bi);
+    if (q == 0) {
+      o[2 + j] = bv;
+      o[2 + K + j] = __int_as_float(bi);
     }
   }
 }
@@ -216,7 +272,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
   if (split8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) b8[k] = ep.bias ? ep.bias[col0 + c8 + k] : 0.f;
-  } else if (ep.bias && c4 < Nlim) {
+  } else if (EPI != EPI_STATS && ep.bias && c4 < Nlim) {  // (EPI_STATS adds the bias per chunk)
 #pragma unroll
     for (int k = 0; k < 4; ++k) b4[k] = ep.bias[col0 + c4 + k];
   }
@@ -229,7 +285,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           *(f32x4*)(L + (r0 + i * 16 + (lane & 15)) * PP_EPI_LDR + wc * (16 * TN) + j * 16 + 4 * (lane >> 4)) =
-              acc[i][j] * acc_scale;
+              EPI == EPI_STATS ? acc[i][j] : acc[i][j] * acc_scale;  // (EPI_STATS scales as it reads)
     }
     __syncthreads();
     const int rows = min(128, Mlim - p * 128);
@@ -243,7 +299,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmEpi& ep, const f32x4 (
     // nothing): a half's stores wait for memory once per batch of rows at
     // most (twice per GELU half), not once per row.
     if constexpr (EPI == EPI_STATS) {
-      pp_stats_rows(ep, L, row0 + p * 128, col0, rows, Nlim, b4, t);
+      pp_stats_rows(ep, L, row0 + p * 128, col0, rows, Nlim, t, acc_scale);
     } else if (split8) {  // GELU columns: 8 per thread, one 16-B store per plane
       constexpr int RPT = 128 / (PP_THREADS / 32);  // rows per thread (8)
       const int rb = t >> 5;

@@ -98,12 +98,14 @@ __global__ void center_rows_kernel(const float* src, float* dst, int rows, int d
 // One wave per row; rows optionally gathered through `row_idx`.  FMT: y is
 // fp32 (ACT_F32) or a planar activation format (split.hpp; ldy counts logical
 // elements); the outputs are bounded by sqrt(d), so no range check.
-constexpr int LN_REG_F4 = 20;  // float4 per lane held in registers: d <= 5120 (Pythia-12B), d % 256 == 0
+// NV: float4 per lane held in registers (10: d <= 2560, 20: d <= 5120, Pythia-12B; d % 256 == 0), else the
+// three-pass loop; LN_G_F4 gamma float4 per lane per group (x2f16 gamma-scaled rows)
+constexpr int LN_G_F4 = 10;
 // g1 (x2f16, engine.hip's exact-fp16 weights): y = LNPre(x) * g1 and, with y2, y2 = LNPre(x) * g2 instead
 // (LN1's and LN2's gamma, or the final LN's alone: the read-in weights' fold_ln scale moved onto the rows),
 // range-checked into flag.
-template <int FMT>
-__global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
+template <int FMT, int NV>
+__global__ void __launch_bounds__(256) lnpre_kernel(const float* __restrict__ x, int ldx,
                              const int32_t* __restrict__ row_idx,
                              void* __restrict__ y, int ldy, int rows, int d,
                              float eps, float2* __restrict__ stats, float* __restrict__ copy = nullptr,
@@ -116,13 +118,30 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
   const int src = row_idx ? row_idx[r] : r;
   const float4* xr = (const float4*)(x + (size_t)src * ldx);
   const int d4 = d >> 2;
-  if (d4 % 64 == 0 && d4 <= 64 * LN_REG_F4) {  // the row in registers: one global read
+  constexpr int LN_REG_F4 = NV;
+  if (NV > 0 && d4 % 64 == 0 && d4 <= 64 * LN_REG_F4) {  // the row in registers: one global read
     const int nv = d4 >> 6;
-    float4 v[LN_REG_F4];
+    float4 v[NV > 0 ? NV : 1];
     float s = 0.f;
 #pragma unroll
     for (int u = 0; u < LN_REG_F4; ++u)
       if (u < nv) v[u] = xr[lane + 64 * u];
+    // the gammas of the x2f16 rows, LN_G_F4 float4 per lane at a time: loaded here, with the row, and not
+    // between the row's stores — vmcnt counts stores too, so a load issued after a store waits for that
+    // store to reach memory, and round 5's per-float4 gamma loads serialised the row into 10 store round
+    // trips (14 us per launch at any row count in the C2 sweeps, profiles/r06/c2_trace_r06h.txt)
+    constexpr int G = NV < LN_G_F4 ? NV : LN_G_F4;
+    [[maybe_unused]] float4 ga[G > 0 ? G : 1], gb[G > 0 ? G : 1];
+    if constexpr (FMT == ACT_X2F16) {
+      if (g1) {
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+          if (u < nv) {
+            ga[u] = ((const float4*)g1)[lane + 64 * u];
+            if (y2) gb[u] = ((const float4*)g2)[lane + 64 * u];
+          }
+      }
+    }
     if (copy && r < copy_rows) {  // the input row itself (a fused sweep's clean rows -> the trace)
       float4* cr = (float4*)(copy + (size_t)r * ldx);
 #pragma unroll
@@ -147,19 +166,31 @@ __global__ void lnpre_kernel(const float* __restrict__ x, int ldx,
       if (g1) {  // the gamma-scaled row(s): y = x g1 (and y2 = x g2 when y2 is given)
         float mx = 0.f;
 #pragma unroll
-        for (int u = 0; u < LN_REG_F4; ++u) {
-          if (u < nv) {
-            const int c = lane + 64 * u;
-            const float4 o = make_float4(v[u].x / scale, v[u].y / scale, v[u].z / scale, v[u].w / scale);
-            const float4 a = ((const float4*)g1)[c];
-            const float4 p = make_float4(o.x * a.x, o.y * a.y, o.z * a.z, o.w * a.w);
-            store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
-            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
-            if (y2) {
-              const float4 b = ((const float4*)g2)[c];
-              const float4 q = make_float4(o.x * b.x, o.y * b.y, o.z * b.z, o.w * b.w);
-              store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
-              mx = fmaxf(mx, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+        for (int g0 = 0; g0 < LN_REG_F4; g0 += G) {
+          if (g0 > 0) {  // the next group's gammas (d > 64 G * 4: one wait for the stores so far)
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+              if (g0 + u < nv) {
+                ga[u] = ((const float4*)g1)[lane + 64 * (g0 + u)];
+                if (y2) gb[u] = ((const float4*)g2)[lane + 64 * (g0 + u)];
+              }
+          }
+#pragma unroll
+          for (int u = 0; u < G; ++u) {
+            if (g0 + u < nv) {
+              const int c = lane + 64 * (g0 + u);
+              const float4 w = v[g0 + u];
+              const float4 o = make_float4(w.x / scale, w.y / scale, w.z / scale, w.w / scale);
+              const float4 a = ga[u];
+              const float4 p = make_float4(o.x * a.x, o.y * a.y, o.z * a.z, o.w * a.w);
+              store_ln4<FMT>((uint16_t*)y + (size_t)r * 2 * ldy + 4 * c, ldy, p.x, p.y, p.z, p.w);
+              mx = fmaxf(mx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
+              if (y2) {
+                const float4 b = gb[u];
+                const float4 q = make_float4(o.x * b.x, o.y * b.y, o.z * b.z, o.w * b.w);
+                store_ln4<FMT>((uint16_t*)y2 + (size_t)r * 2 * ldy + 4 * c, ldy, q.x, q.y, q.z, q.w);
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+              }
             }
           }
         }
