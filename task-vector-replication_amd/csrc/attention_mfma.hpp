@@ -392,6 +392,24 @@ struct RowAttnShape {
   static constexpr int LPH = DH / E;            // lanes per head
 };
 
+// E consecutive floats at a 4-B-aligned address as 16-B loads + the rest (global_load_dwordx4 needs only
+// dword alignment): a lane's E = 5 dims were five 4-B loads, each instruction touching all 20 lines of the
+// wave's 1,280-B span — the kernel ran at the TA's line rate (C2: 30 us per launch at 1,768 rows)
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+template <int E>
+__device__ __forceinline__ void load_span(const float* __restrict__ p, float (&x)[E]) {
+#pragma unroll
+  for (int i = 0; i + 4 <= E; i += 4) {
+    const f32x4u v = *(const f32x4u*)(p + i);
+    x[i] = v[0];
+    x[i + 1] = v[1];
+    x[i + 2] = v[2];
+    x[i + 3] = v[3];
+  }
+#pragma unroll
+  for (int i = E & ~3; i < E; ++i) x[i] = p[i];
+}
+
 template <int FMT, int DH>
 __global__ void __launch_bounds__(256)
 attention_row_kernel(const float* __restrict__ qkv, int ldq, const float* __restrict__ cache, int ldc,
@@ -422,18 +440,16 @@ attention_row_kernel(const float* __restrict__ qkv, int ldq, const float* __rest
     for (int i = 0; i < E; ++i) p[i] = __shfl_xor(x[i], OFF, 64);  // every lane, before any divergence
     if (e < 2 * OFF) {
       const float sg = (e & OFF) == 0 ? -1.f : 1.f;  // x0 cos - x1 sin | x1 cos + x0 sin
+      float cs[E], sn[E];
+      load_span<E>(cos_t + pos * rd + e * E, cs);
+      load_span<E>(sin_t + pos * rd + e * E, sn);
 #pragma unroll
-      for (int i = 0; i < E; ++i) {
-        const int dim = e * E + i;
-        x[i] = x[i] * cos_t[pos * rd + dim] + sg * p[i] * sin_t[pos * rd + dim];
-      }
+      for (int i = 0; i < E; ++i) x[i] = x[i] * cs[i] + sg * p[i] * sn[i];
     }
   };
   float q[E];
   {
-    const float* r = row_of(qpos) + col;
-#pragma unroll
-    for (int i = 0; i < E; ++i) q[i] = r[i];
+    load_span<E>(row_of(qpos) + col, q);
     rotate(q, qpos);
   }
   float m_run = -INFINITY, l_run = 0.f, acc[E];
@@ -446,11 +462,8 @@ attention_row_kernel(const float* __restrict__ qkv, int ldq, const float* __rest
     for (int u = 0; u < KB; ++u) {
       const int j = min(j0 + u, T - 1);
       const float* r = row_of(j);
-#pragma unroll
-      for (int i = 0; i < E; ++i) {
-        kv[u][i] = r[d + col + i];
-        vv[u][i] = r[2 * d + col + i];
-      }
+      load_span<E>(r + d + col, kv[u]);
+      load_span<E>(r + 2 * d + col, vv[u]);
     }
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
@@ -474,15 +487,25 @@ attention_row_kernel(const float* __restrict__ qkv, int ldq, const float* __rest
   }
   const size_t zrow = (size_t)(sd.row0 + sd.n - 1);
   const float inv = 1.0f / l_run;
+  // z through a per-wave LDS row: lane l's E dims at 4 l E B would go out as E 2-B (planes) or 4-B stores
+  // per lane, each instruction touching the whole span's lines; re-read as 4 consecutive dims per lane
+  // they go out as 8-B plane / 16-B fp32 stores
+  __shared__ __attribute__((aligned(16))) float zs[4][HG * DH];
+  float* zw = zs[(threadIdx.x >> 6) & 3];
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const float v = acc[i] * inv;
+  for (int i = 0; i < E; ++i) zw[lane * E + i] = acc[i] * inv;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int c0 = h0 * DH;
+  for (int c = 4 * lane; c < HG * DH; c += 256) {
+    const f32x4 v = *(const f32x4*)(zw + c);
     if constexpr (FMT != ACT_F32)
-      store_act<FMT>((uint16_t*)z + zrow * 2 * ldz + col + i, ldz, v, flag);
+      store_act4<FMT>((uint16_t*)z + zrow * 2 * ldz + c0 + c, ldz, v[0], v[1], v[2], v[3], flag);
     else
-      ((float*)z)[zrow * ldz + col + i] = v;
-    if (zf && zf_last) zf[(size_t)s * ldzf + col + i] = v;  // the capture's compact last-row copy
-    else if (zf && zrow < (size_t)zf_rows) zf[zrow * ldzf + col + i] = v;
+      *(f32x4u*)((float*)z + zrow * ldz + c0 + c) = v;
+    if (zf && zf_last) *(f32x4u*)(zf + (size_t)s * ldzf + c0 + c) = v;  // the capture's compact last-row copy
+    else if (zf && zrow < (size_t)zf_rows) *(f32x4u*)(zf + zrow * ldzf + c0 + c) = v;
   }
 }
 
