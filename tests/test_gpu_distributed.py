@@ -141,3 +141,55 @@ def test_c5_leg_two_ranks_equals_one_process(tmp_path):
         err = (got["cie"].double() - cie1).abs().max().item()
         print(f"C5 rehearsal rank {r}: |sharded - one process| {err:.2e} of max |CIE sum| {big:.3e}")
         assert err <= 1e-5 * big + 1e-9, (r, err, big)
+
+
+def _rccl_worker(init, q):
+    """One rank on the RCCL backend (torch's "nccl" is RCCL on ROCm), bound to cuda:0 as bench.py binds its
+    ranks (device_id): the sharded CIE and extraction, whose collectives then run on device tensors through
+    RCCL, plus an explicit all_reduce / all_gather / broadcast."""
+    import torch.distributed as dist
+    os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=init, rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        assert dist.get_backend() == "nccl"
+        out = _run(True)
+        t = torch.arange(8, dtype=torch.float32, device="cuda") + 1
+        dist.all_reduce(t)
+        g = [torch.empty_like(t)]
+        dist.all_gather(g, t)
+        dist.broadcast(t, 0)
+        torch.cuda.synchronize()
+        out["coll"] = (t.cpu(), g[0].cpu())
+        q.put(out)
+    except Exception as e:
+        q.put(repr(e))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_rccl_one_rank_on_the_engine(tmp_path):
+    """The `nccl` (RCCL) branch bench.py takes on a multi-GPU node, executed on this box's one GPU at world
+    size 1: init with device_id, the sharded entry points' collectives on device tensors, and the results
+    equal the unsharded engine's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(f"file://{tmp_path / 'rccl'}", q))
+    p.start()
+    try:
+        got = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert isinstance(got, dict), got
+    ref = _run(False)
+    # (the same sites, possibly batched and split-K-planned differently: fp32 rounding only, as the 2-rank test)
+    assert torch.allclose(got["cie"], ref["cie"], rtol=0, atol=1e-6 * ref["cie"].abs().max().item() + 1e-9)
+    assert torch.allclose(got["mean"], ref["mean"], rtol=1e-5, atol=1e-6 * ref["mean"].abs().max().item())
+    assert got["acc"] == ref["acc"] and got["fv"] == ref["fv"]
+    assert torch.allclose(got["dprob"], ref["dprob"], rtol=0, atol=1e-6)
+    t, g = got["coll"]
+    assert torch.equal(t, torch.arange(8, dtype=torch.float32) + 1) and torch.equal(g, t)

@@ -119,3 +119,26 @@ def test_replan_on_the_model_device(tiny_cfg, tokenizer):
         assert torch.cuda.current_device() == 0
     b = model.forward_clean(ids, return_logits=True)["logits"]
     assert torch.equal(a, b)
+
+
+def test_replan_round_trip_one_device(tiny_cfg, tokenizer):
+    """The one-GPU form of the test above: exact16 off / on and x3bf16 / x2f16 re-plans come back to the same
+    binding bit for bit (the x2f16 planes rebuilt from the kept weights), the mode mirrors follow the engine,
+    and the current device is unchanged."""
+    sd = tvr_amd.weights.synth_hf_state_dict(tiny_cfg, seed=0, std=0.15, fp16=True)
+    model = tvr_amd.Model.from_hf_state_dict(tiny_cfg, sd, device="cuda:0", tokenizer=tokenizer, gemm="x2f16")
+    ids = [[0, 5, 7, 9, 11], [0, 3, 2]]
+    a = model.forward_clean(ids, return_logits=True)["logits"]
+    dev = torch.cuda.current_device()
+    model.set_exact16(False)
+    assert not model.exact16 and model.gemm == "x2f16"
+    p = model.forward_clean(ids, return_logits=True)["logits"]
+    assert (p - a).abs().max().item() <= 1e-5 * a.abs().max().item()  # processed weights: fp32-level agreement
+    model.set_gemm("x3bf16")
+    assert model.gemm == "x3bf16"
+    model.set_gemm("x2f16")
+    model.set_exact16(True)
+    assert model.exact16 and model.gemm == "x2f16"
+    assert torch.cuda.current_device() == dev
+    b = model.forward_clean(ids, return_logits=True)["logits"]
+    assert torch.equal(a, b)
