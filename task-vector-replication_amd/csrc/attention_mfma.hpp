@@ -35,6 +35,44 @@ namespace tvr {
 
 constexpr int ATTM_WAVES = 4;  // (sequence, head) pairs per block
 
+// E consecutive floats at a 4-B-aligned address as 16-B loads + the rest (global_load_dwordx4 needs only
+// dword alignment): a lane's E = 5 dims were five 4-B loads, each instruction touching all 20 lines of the
+// wave's 1,280-B span — the kernel ran at the TA's line rate (C2: 30 us per launch at 1,768 rows)
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+template <int E>
+__device__ __forceinline__ void load_span(const float* __restrict__ p, float (&x)[E]) {
+#pragma unroll
+  for (int i = 0; i + 4 <= E; i += 4) {
+    const f32x4u v = *(const f32x4u*)(p + i);
+    x[i] = v[0];
+    x[i + 1] = v[1];
+    x[i + 2] = v[2];
+    x[i + 3] = v[3];
+  }
+#pragma unroll
+  for (int i = E & ~3; i < E; ++i) x[i] = p[i];
+}
+
+// The P V product's dimension order (TVR_ATT_VPERM, default 0).  Output tile dt of Z^T = V^T P^T holds the
+// dims d(i, dt) of its 16 rows i: 0 -> d = 16 dt + i (NDT 4-B loads per key row and lane, 64 B per row per
+// instruction; a lane's z values are 4-dim groups 16 dt + 4 g, so a store instruction writes 32-B (planes)
+// / 64-B (fp32) row runs); 1 -> d = NDT i + dt, so lane (li, g) reads the NDT CONSECUTIVE floats
+// V[key][NDT li ..] of a key row (16-B loads) and ends with the DH / 4 consecutive dims [g DH / 4, (g + 1)
+// DH / 4) of its query, whose direct stores are 8-B pieces 64 B apart.  Every output element sums the same
+// products over the same keys in the same order either way (bit-identical), but 1 measured slower where z is
+// stored from registers: 12B (NKT 4, d_head 128) 4,278 vs 3,810 us per launch, 6.9B (STAGE 3) 2,524 vs
+// 2,410; C3 (STAGE 2, z through LDS) 701 vs 702 (profiles/r06/attention_vperm_ab_r06s2c.txt)
+#ifndef TVR_ATT_VPERM
+#define TVR_ATT_VPERM 0
+#endif
+constexpr bool ATT_VPERM = TVR_ATT_VPERM;
+// Unstaged kernels with two or more key tiles (ZL, TVR_ATT_ZLDS): z leaves through a per-wave [16][DH] LDS
+// region as the staged forms do (whole-row 16-B stores per plane) instead of one 8-B (planes) / 16-B (fp32)
+// store per lane and 4-dim group
+#ifndef TVR_ATT_ZLDS
+#define TVR_ATT_ZLDS 0
+#endif
+
 // grid = ceil(n_seqs * n_heads / ATTM_WAVES) blocks of 64 * ATTM_WAVES threads;
 // NKT = key tiles the launch's longest sequence needs (1, 2, 4 or 8: the
 // register arrays are sized by it), or 0 for longer sequences (up to n_ctx):
@@ -76,7 +114,8 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   constexpr int SMAT = 16 * DH;  // floats of one staged [16][DH] matrix
   // staged matrices (STAGE 3: V's two key tiles); K's offset
   constexpr int NMAT = STAGE == 1 ? 3 : 2, KOFF = STAGE == 1 ? SMAT : 0;
-  __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * NMAT * SMAT : 4];
+  constexpr bool ZL = TVR_ATT_ZLDS && STAGE == 0 && NKT != 1;  // z through a per-wave [16][DH] region
+  __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * NMAT * SMAT : ZL ? ATTM_WAVES * SMAT : 4];
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);
   if (pair >= n_seqs * n_heads) return;  // a whole wave; nothing below synchronises
@@ -114,7 +153,17 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     }
   };
 
-  float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * NMAT * SMAT : 0);
+  // the lane's NDT A-operand values of the P V product from V row vrow (&V[key][h DH], global or staged)
+  auto load_v = [&](const float* vrow, float (&x)[NDT]) {
+    if constexpr (ATT_VPERM) {
+      load_span<NDT>(vrow + NDT * li, x);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) x[dt] = vrow[16 * dt + li];
+    }
+  };
+
+  float* stg = att_lds + (STAGE ? (threadIdx.x >> 6) * NMAT * SMAT : ZL ? (threadIdx.x >> 6) * SMAT : 0);
   if constexpr (STAGE == 3) {
     // V's rows 0 .. 31 (clamped to T - 1) as a packed [32][DH] image, issued before Q and K are loaded so
     // its latency hides behind theirs and the QK^T / softmax; waited for (vmcnt) before the first PV MFMA
@@ -212,10 +261,11 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
           if (kb + kt < kt_end) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float* vr = row_of(min(16 * (kb + kt) + 4 * g + r, T - 1)) + 2 * d + h * DH + li;
+              float vf[NDT];
+              load_v(row_of(min(16 * (kb + kt) + 4 * g + r, T - 1)) + 2 * d + h * DH, vf);
 #pragma unroll
               for (int dt = 0; dt < NDT; ++dt)
-                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[dt], st[kt][r], zt[dt], 0, 0, 0);
             }
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -232,18 +282,21 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
       if constexpr (NKT == 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float* vr = STAGE ? stg + KOFF + SMAT + (4 * g + r) * DH + li
-                                  : row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH + li;
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) vpre[r][dt] = vr[16 * dt];
+          load_v(STAGE ? stg + KOFF + SMAT + (4 * g + r) * DH : row_of(min(4 * g + r, T - 1)) + 2 * d + h * DH,
+                 vpre[r]);
         }
       }
 
+      // causal key tiles of this query tile: through its last row's position.  A tile past it is masked for
+      // every query of the tile (exp(-inf) = 0 in the softmax, P V adds exact zeros), so skipping its QK^T
+      // and PV products leaves every result bit-identical (the LONG path's kt_end): at T = 33 (C5) the three
+      // query tiles need 1 / 2 / 3 key tiles, 6 of the 9 products; at T = 23 (C4) 3 of 4
+      const int nkq = min(nkt, (sd.p0 + min(q0 + 15, sd.n - 1)) / 16 + 1);
       f4 st[MAXKT];
 #pragma unroll
       for (int kt = 0; kt < MAXKT; ++kt) {
         st[kt] = f4{0.f, 0.f, 0.f, 0.f};
-        if (kt < nkt) {
+        if (kt < nkq) {
           const int kj = min(16 * kt + li, T - 1);
           float kf[CH];
           if constexpr (STAGE == 1 || STAGE == 2)
@@ -270,7 +323,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = 16 * kt + 4 * g + r;
-          const float v = (kt < nkt && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
+          const float v = (kt < nkq && key <= qpos && key < T) ? st[kt][r] * inv_attn_scale : -INFINITY;
           st[kt][r] = v;
           mx = fmaxf(mx, v);
         }
@@ -300,7 +353,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
       for (int dt = 0; dt < NDT; ++dt) zt[dt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < MAXKT; ++kt) {
-        if (kt < nkt) {
+        if (kt < nkq) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             if constexpr (NKT == 1) {
@@ -308,26 +361,42 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
               for (int dt = 0; dt < NDT; ++dt)
                 zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vpre[r][dt], st[kt][r], zt[dt], 0, 0, 0);
             } else if constexpr (STAGE == 3) {
-              const float* vr = stg + (16 * kt + 4 * g + r) * DH + li;  // staged row = key min(., T - 1)
+              float vf[NDT];
+              load_v(stg + (16 * kt + 4 * g + r) * DH, vf);  // staged row = key min(., T - 1)
 #pragma unroll
               for (int dt = 0; dt < NDT; ++dt)
-                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[dt], st[kt][r], zt[dt], 0, 0, 0);
             } else {
-              const float* vr = row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH + li;  // P = 0 past T
+              float vf[NDT];
+              load_v(row_of(min(16 * kt + 4 * g + r, T - 1)) + 2 * d + h * DH, vf);  // P = 0 past T
 #pragma unroll
               for (int dt = 0; dt < NDT; ++dt)
-                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[16 * dt], st[kt][r], zt[dt], 0, 0, 0);
+                zt[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[dt], st[kt][r], zt[dt], 0, 0, 0);
             }
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (STAGE == 1 || STAGE == 2) {
-      // z through the wave's first staged region (Q or K: read above): then each lane stores 8 consecutive dims of one
-      // row (one 16-B store per plane), so a row's DH dims leave as one contiguous run per plane
+    // the lane's output in 4-dim groups c: VPERM dims g DH / 4 + 4 c .. + 3 (zt[dt][r] is dim NDT (4 g + r) + dt),
+    // else dims 16 c + 4 g .. + 3 (zt[c])
+    auto zgroup = [&](int c) -> f4 {
+      if constexpr (ATT_VPERM) {
+        f4 v;
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) *(f4*)(stg + li * DH + 16 * dt + 4 * g) = zt[dt];
+        for (int e = 0; e < 4; ++e) v[e] = zt[(4 * c + e) % NDT][(4 * c + e) / NDT];
+        return v;
+      } else {
+        return zt[c];
+      }
+    };
+    auto zcol = [&](int c) { return ATT_VPERM ? g * (DH / 4) + 4 * c : 16 * c + 4 * g; };
+    if constexpr (STAGE == 1 || STAGE == 2 || ZL) {
+      // z through the wave's first staged region (Q or K: read above; ZL its own): then each lane stores 8 consecutive
+      // dims of one row (one 16-B store per plane), so a row's DH dims leave as one contiguous run per plane
+      if constexpr (ZL) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous query tile's z reads
+#pragma unroll
+      for (int c = 0; c < NDT; ++c) *(f4*)(stg + li * DH + zcol(c)) = zgroup(c);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       constexpr int C8 = DH / 8;  // 8-dim chunks per row
       for (int id = lane; id < 16 * C8; id += 64) {
@@ -355,9 +424,9 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
     } else if (q0 + li < sd.n) {
       const size_t zrow = (size_t)(sd.row0 + q0 + li);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const int col = h * DH + 16 * dt + 4 * g;
-        const f4 v = zt[dt];
+      for (int c = 0; c < NDT; ++c) {
+        const int col = h * DH + zcol(c);
+        const f4 v = zgroup(c);
         if constexpr (FMT != ACT_F32)
           store_act4<FMT>((uint16_t*)z + zrow * 2 * ldz + col, ldz, v[0], v[1], v[2], v[3], flag);
         else
@@ -391,24 +460,6 @@ struct RowAttnShape {
   static constexpr int E = HG * DH / 64;        // dims per lane (16: 1, 64: 4, 80: 5, 128: 4)
   static constexpr int LPH = DH / E;            // lanes per head
 };
-
-// E consecutive floats at a 4-B-aligned address as 16-B loads + the rest (global_load_dwordx4 needs only
-// dword alignment): a lane's E = 5 dims were five 4-B loads, each instruction touching all 20 lines of the
-// wave's 1,280-B span — the kernel ran at the TA's line rate (C2: 30 us per launch at 1,768 rows)
-typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
-template <int E>
-__device__ __forceinline__ void load_span(const float* __restrict__ p, float (&x)[E]) {
-#pragma unroll
-  for (int i = 0; i + 4 <= E; i += 4) {
-    const f32x4u v = *(const f32x4u*)(p + i);
-    x[i] = v[0];
-    x[i + 1] = v[1];
-    x[i + 2] = v[2];
-    x[i + 3] = v[3];
-  }
-#pragma unroll
-  for (int i = E & ~3; i < E; ++i) x[i] = p[i];
-}
 
 template <int FMT, int DH>
 __global__ void __launch_bounds__(256)
