@@ -66,11 +66,12 @@ __device__ __forceinline__ void load_span(const float* __restrict__ p, float (&x
 #define TVR_ATT_VPERM 0
 #endif
 constexpr bool ATT_VPERM = TVR_ATT_VPERM;
-// Unstaged kernels with two or more key tiles (ZL, TVR_ATT_ZLDS): z leaves through a per-wave [16][DH] LDS
-// region as the staged forms do (whole-row 16-B stores per plane) instead of one 8-B (planes) / 16-B (fp32)
-// store per lane and 4-dim group
+// Unstaged kernels (ZL, TVR_ATT_ZLDS, default 1): z leaves through a per-wave [16][DH] LDS region (8 KB at
+// d_head 128) as the staged forms do — whole-row 16-B stores per plane — instead of one 8-B (planes) /
+// 16-B (fp32) store per lane and 4-dim group, 32-B row runs per instruction: 12B (NKT 4, d_head 128)
+// 3,819 / 3,735 -> 3,449 / 3,451 us per launch, same box (profiles/r06/attention_zlds_ab_r06s2d.txt)
 #ifndef TVR_ATT_ZLDS
-#define TVR_ATT_ZLDS 0
+#define TVR_ATT_ZLDS 1
 #endif
 
 // grid = ceil(n_seqs * n_heads / ATTM_WAVES) blocks of 64 * ATTM_WAVES threads;
@@ -114,7 +115,7 @@ attention_mfma_kernel(const float* __restrict__ qkv, int ldq, const float* __res
   constexpr int SMAT = 16 * DH;  // floats of one staged [16][DH] matrix
   // staged matrices (STAGE 3: V's two key tiles); K's offset
   constexpr int NMAT = STAGE == 1 ? 3 : 2, KOFF = STAGE == 1 ? SMAT : 0;
-  constexpr bool ZL = TVR_ATT_ZLDS && STAGE == 0 && NKT != 1;  // z through a per-wave [16][DH] region
+  constexpr bool ZL = TVR_ATT_ZLDS && STAGE == 0;  // z through a per-wave [16][DH] region
   __shared__ __attribute__((aligned(16))) float att_lds[STAGE ? ATTM_WAVES * NMAT * SMAT : ZL ? ATTM_WAVES * SMAT : 4];
   const int lane = threadIdx.x & 63;
   const int pair = blockIdx.x * ATTM_WAVES + (threadIdx.x >> 6);

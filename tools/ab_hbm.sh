@@ -2,15 +2,17 @@
 # HBM-bound kernels' launch times (hbm_kernels: entry / lnpre / attention / lin_entry); lines to
 # gpurun_out/ab_<tag>/summary.txt.
 #   gpurun -- 'bash tools/ab_hbm.sh <tag> <rounds> <libA.so,libB.so[,...]> [extra bench args]'
+# A variant may carry env knobs: VAR=v+VAR2=w:lib.so
 set -o pipefail
 TAG=${1:?tag}; ROUNDS=${2:?rounds}; LIBS=${3:?libs}; shift 3
 export TMPDIR=/tmp
 OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
-  for lib in ${LIBS//,/ }; do
-    n=$(basename $(dirname $lib))_$(basename $lib .so)_$r
-    TVR_LIB=$lib timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg \
+  for var in ${LIBS//,/ }; do
+    lib=${var##*:}; ev=""; [ "$lib" != "$var" ] && ev=${var%:*}
+    n=$(basename $(dirname $lib))_$(basename $lib .so)${ev:+_${ev//[=+]/_}}_$r
+    env ${ev//+/ } TVR_LIB=$lib timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-leg \
         --no-processed-leg --extract 0 --configs= "$@" > $OUT/$n.json 2> $OUT/$n.err || { tail -5 $OUT/$n.err; exit 1; }
     python3 -c "
 import json, sys
