@@ -101,13 +101,39 @@ __global__ void lin_planes_kernel(const float* __restrict__ s, int N, int H, int
 // the QKV + MLP-in epilogue does: Q|K|V fp32 to qkv, GELU(h) in the
 // activation format to the a2 columns after z.
 constexpr int LIN_LDR = 260;  // floats per LDS row (conflict-free 16-B writes of the 16 x 16 fragments)
+// Occupancy (round 6): the block was held to 2 per CU by both its LDS tile (66 KB) and its registers (221),
+// i.e. 8 waves per CU for a latency-bound kernel.  Now the tile goes through LDS in two 128-column passes
+// (TVR_LIN_HALVES 2: 35 KB), the product's z / Wsc loads are single-buffered (TVR_LIN_SB 1) and the combine
+// issues the loads of 4 rows at a time (TVR_LIN_RB), so the kernel fits 168 VGPRs without spills: 3 waves per
+// SIMD (TVR_LIN_WAVES).  C3 341.5 / 341.8 -> 327.6 / 328.2 us per launch (0.43 -> 0.45 of HBM), 12B 1,128 ->
+// 1,072, same box; the halves alone (2 waves / SIMD, one more barrier) 465 us
+// (profiles/r06/lin_entry_occupancy_ab_r06s2l.txt).  A/B: -DTVR_LIN_HALVES=1 -DTVR_LIN_SB=0 -DTVR_LIN_WAVES=0
+// -DTVR_LIN_RB=8 (round 5's form)
+#ifndef TVR_LIN_HALVES
+#define TVR_LIN_HALVES 2
+#endif
+#ifndef TVR_LIN_SB
+#define TVR_LIN_SB 1
+#endif
+#ifndef TVR_LIN_WAVES
+#define TVR_LIN_WAVES 3
+#endif
+#ifndef TVR_LIN_RB
+#define TVR_LIN_RB 4  // rows per combine batch (their y_c / G loads issued together)
+#endif
+constexpr int LIN_HALVES = TVR_LIN_HALVES;
 // NK = KP / 32 k-steps, fully unrolled with the next step's z / Wsc loads
 // issued before this step's MFMAs.  1-D grid of n_mb x column tiles with the
 // XCD-aware bijective remap (gemm_pingpong.hpp): the m-blocks that share a
 // head's Wsc tile are consecutive work items, so they run on one XCD together
 // and read that tile from one L2.
 template <int FMT, int NK>
-__global__ void __launch_bounds__(LIN_THREADS)
+__global__ void
+#if TVR_LIN_WAVES > 0
+__launch_bounds__(LIN_THREADS, TVR_LIN_WAVES)
+#else
+__launch_bounds__(LIN_THREADS)
+#endif
 lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restrict__ rows,
                  const uint16_t* __restrict__ wp, size_t wps, float acc_scale, const float* __restrict__ z, int d,
                  int dh, const float2* __restrict__ stats, float* __restrict__ qkv, const float* __restrict__ raw_h,
@@ -116,7 +142,8 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
                  int ct_base = 0) {
   using frag = typename PlanarFmt<FMT>::frag;
   constexpr int KP = 32 * NK;
-  __shared__ __attribute__((aligned(16))) float tile[64 * LIN_LDR];
+  constexpr int CW = 256 / LIN_HALVES, LDR = LIN_HALVES == 1 ? LIN_LDR : CW + 4;  // columns per LDS pass, row stride
+  __shared__ __attribute__((aligned(16))) float tile[64 * LDR];
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int mbi = work % n_mb, ct = work / n_mb;
@@ -135,7 +162,12 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
     rcoef[threadIdx.x] = f32x4{sc.y * inv, (sc.x - st.x) * inv, inv, 0.f};
     rrow[threadIdx.x] = make_int4(q.out_row, q.clean_row, q.vrow, 0);
   }
-  if (nb < N) {  // (a wave past N skips the product but joins the barrier)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+  if (nb < N) {  // (a wave past N skips the product but joins the barriers)
     const float* zr[4];
     bool live[4];
 #pragma unroll
@@ -146,14 +178,10 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
     const uint16_t* wr[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr[j] = wp + ((size_t)mb.head * N + min(nb + 16 * j + r16, N - 1)) * KP + 8 * g;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
     // raw loads of k-step s (lane: 8 k values at 32 s + 8 g; dh % 16 == 0: a chunk is wholly in or out)
-    f32x4 zx[2][4], zy[2][4];
-    frag w0[2][4], w1[2][4];
+    constexpr int NB = TVR_LIN_SB ? 1 : 2;  // load buffers
+    f32x4 zx[NB][4], zy[NB][4];
+    frag w0[NB][4], w1[NB][4];
     auto load = [&](int s, int b) {
       const bool kin = 32 * s + 8 * g < dh;
 #pragma unroll
@@ -171,11 +199,14 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
         if constexpr (FMT == ACT_X2F16) w1[b][j] = *(const frag*)(wr[j] + 32 * s + wps);
       }
     };
-    load(0, 0);
+    if (NB == 2) load(0, 0);
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      const int b = s & 1;
-      if (s + 1 < NK) load(s + 1, b ^ 1);
+      const int b = NB == 2 ? s & 1 : 0;
+      if (NB == 1)
+        load(s, 0);
+      else if (s + 1 < NK)
+        load(s + 1, b ^ 1);
       frag a0[4], a1[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -212,23 +243,29 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
           acc[i][j] = c;
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *(f32x4*)(tile + (16 * i + r16) * LIN_LDR + wave * 64 + 16 * j + 4 * g) = acc[i][j] * acc_scale;
   }
-  __syncthreads();
   // combine + store: thread t takes columns col0 + 4 (t & 63) .. +3 of rows t >> 6, + 4, ...
   // in batches of 8 rows whose y_c / G loads are all issued before the batch's
   // stores (qkv is read at clean rows and written at entering rows, so the
   // compiler may not move a load past a store; one load after a store would
   // make it wait for that store to reach memory: s_waitcnt vmcnt counts both).
-  const int cl = 4 * (threadIdx.x & 63), n0 = col0 + cl, n3 = 3 * d;
-  if (n0 >= N) return;
+  // (LIN_HALVES 2: the same per column pass; the waves whose 64 columns lie in the pass write them first)
+  constexpr int TPR = CW / 4, RS = LIN_THREADS / TPR, RB = TVR_LIN_RB;  // threads per row, rows per step, rows per batch
+  const int cl = 4 * (threadIdx.x % TPR), n3 = 3 * d;
+  for (int hf = 0; hf < LIN_HALVES; ++hf) {
+  if (hf > 0) __syncthreads();  // the previous pass's tile reads are done
+  if (nb < N && (wave * 64) / CW == hf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(f32x4*)(tile + (16 * i + r16) * LDR + (wave * 64) % CW + 16 * j + 4 * g) = acc[i][j] * acc_scale;
+  }
+  __syncthreads();
+  const int n0 = col0 + hf * CW + cl;
+  if (n0 >= N) continue;
   const f32x4 b = *(const f32x4*)(b1 + n0), c = *(const f32x4*)(c1 + n0);
-  constexpr int RB = 8, RS = LIN_THREADS / 64;
-  for (int r0 = threadIdx.x >> 6; r0 < mb.rows; r0 += RS * RB) {
+  for (int r0 = threadIdx.x / TPR; r0 < mb.rows; r0 += RS * RB) {
     int4 q[RB];
     f32x4 yc[RB], gv[RB];
 #pragma unroll
@@ -243,7 +280,7 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
       const int r = r0 + RS * i;
       if (r >= mb.rows) break;
       const f32x4 k = rcoef[r];
-      const f32x4 v = *(const f32x4*)(tile + r * LIN_LDR + cl);
+      const f32x4 v = *(const f32x4*)(tile + r * LDR + cl);
       f32x4 y;
 #pragma unroll
       for (int e = 0; e < 4; ++e) y[e] = k[0] * (yc[i][e] - b[e]) + k[1] * c[e] + k[2] * (gv[i][e] - v[e]) + b[e];
@@ -254,6 +291,7 @@ lin_entry_kernel(const LinMB* __restrict__ mbs, int n_mb, const LinRow* __restri
         store_act4<FMT>(out1h + (size_t)q[i].x * ld1h + (n0 - n3), ps1h, g01.x, g01.y, g23.x, g23.y, range_flag);
       }
     }
+  }
   }
 }
 
